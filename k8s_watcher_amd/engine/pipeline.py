@@ -1,0 +1,165 @@
+"""The per-event pipeline (SURVEY C9 ``handle_pod_event``, §3.2 hot loop).
+
+Order of operations matches ``/root/reference/watcher/pod_watcher.py:214-241``:
+
+1. production ``critical_events_only`` filter — silent drop (``:220-221``);
+2. INFO ``Pod event detected: <TYPE> - <ns>/<name>`` (``:223``) — logged
+   *before* the namespace filter, as in the reference;
+3. client-side namespace filter with DEBUG ``Skipping pod ...`` (``:226-229``);
+4. payload build + ``event_type`` (``:232-233``);
+5. notify (commented out in the reference, ``:236``; enabled here).
+
+Additions: every event first updates the pod cache (for ``notify_on:
+phase_change`` and relist diffs), and events are processed in *batches* —
+all events decoded from one socket read share one pass, one timestamp and
+one notifier flush, which is what keeps Python overhead per event small.
+"""
+
+from __future__ import annotations
+
+import logging
+from typing import List, Optional
+
+from ..metrics import Metrics
+from ..ops.cache import CORE, MISSING, NAME, NS, PHASE, PodCache
+from ..ops.decode import (ADDED, BOOKMARK, DELETED, E_EXTRA, E_HAS_STATUS, E_NAME, E_NS, E_PHASE,
+                          E_RV, E_TYPE, E_UID, MODIFIED)
+from ..ops.filters import TERMINAL_PHASES
+from ..utils.config import Settings
+from ..utils.logsetup import SERVICE_LOGGER
+from ..utils.timefmt import event_timestamp
+
+_POD_EVENTS = frozenset({ADDED, MODIFIED, DELETED})
+
+
+class EventPipeline:
+    def __init__(self, settings: Settings, decoder, notifier, metrics: Metrics,
+                 cache: Optional[PodCache] = None) -> None:
+        w = settings.watcher
+        self.settings = settings
+        self.decoder = decoder
+        self.notifier = notifier
+        self.metrics = metrics
+        self.cache = cache if cache is not None else PodCache()
+        self.log = logging.getLogger(SERVICE_LOGGER)
+        self.critical_active = settings.environment == "production" and w.critical_events_only
+        self.namespaces = frozenset(w.namespaces)
+        self.phase_mode = w.notify_on == "phase_change"
+        self.ts_mode = w.event_timestamp
+        self.log_events_setting = w.log_events
+        self.last_rv: Optional[str] = None
+
+    @property
+    def log_events(self) -> bool:
+        if self.log_events_setting is not None:
+            return self.log_events_setting
+        return self.log.isEnabledFor(logging.INFO)
+
+    def handle_batch(self, events: List[tuple], read_ns: int) -> List[tuple]:
+        """Process decoded events; returns control events (ERROR/INVALID) for the reflector."""
+        ctrl: List[tuple] = []
+        c = self.metrics.c
+        entries = self.cache.entries
+        critical = self.critical_active
+        nsset = self.namespaces
+        phase_mode = self.phase_mode
+        log = self.log
+        log_events = self.log_events
+        log_debug = log_events and log.isEnabledFor(logging.DEBUG)
+        decoder = self.decoder
+        submit = self.notifier.submit
+        ts = None
+        for ev in events:
+            et = ev[E_TYPE]
+            if et not in _POD_EVENTS:
+                if et == BOOKMARK:
+                    if ev[E_RV]:
+                        self.last_rv = ev[E_RV]
+                    c["bookmarks"] += 1
+                else:
+                    ctrl.append(ev)
+                continue
+            c["events_received"] += 1
+            uid = ev[E_UID]
+            rv = ev[E_RV]
+            if rv:
+                self.last_rv = rv
+            phase = ev[E_PHASE]
+            ns = ev[E_NS]
+            name = ev[E_NAME]
+            # cache update (inline PodCache.observe for speed)
+            ent = entries.get(uid)
+            prev = MISSING if ent is None else ent[PHASE]
+            if et == DELETED:
+                if ent is not None:
+                    del entries[uid]
+            elif ent is None:
+                ent = [rv, phase, ns, name, None]
+                entries[uid] = ent
+            else:
+                ent[0] = rv
+                ent[PHASE] = phase
+            if critical and not (et == DELETED or not ev[E_HAS_STATUS] or phase in TERMINAL_PHASES):
+                c["events_filtered_critical"] += 1
+                continue
+            if log_events:
+                log.info("Pod event detected: %s - %s/%s", et, ns, name)
+            if nsset and ns not in nsset:
+                if log_debug:
+                    log.debug("Skipping pod %s/%s - not in target namespaces", ns, name)
+                c["events_filtered_namespace"] += 1
+                continue
+            if phase_mode and not (et == DELETED or prev is MISSING or prev != phase):
+                c["events_unchanged"] += 1
+                continue
+            core = ev[E_EXTRA]
+            if core is None:
+                core = decoder.core(ev)
+            if et != DELETED:
+                ent[CORE] = core
+            if ts is None:
+                ts = event_timestamp(self.ts_mode)
+            submit(uid, et, ns, name, core, read_ns, ts)
+        self.notifier.flush()
+        return ctrl
+
+    # ------------------------------------------------------------------ relist
+    def reconcile(self, listed: List[tuple], read_ns: int, notify: bool = True,
+                  scope_ns: Optional[str] = None) -> List[tuple]:
+        """Diff a full LIST against the cache and run the resulting events.
+
+        New uid → ADDED, changed resourceVersion → MODIFIED, cached uid absent
+        from the list → DELETED (payload from the last cached core). With
+        ``notify=False`` the cache is primed silently (``initial_list: skip``).
+        ``scope_ns`` limits deletions to one namespace (server-side scopes).
+        """
+        entries = self.cache.entries
+        out: List[tuple] = []
+        seen = set()
+        for ev in listed:
+            uid = ev[E_UID]
+            seen.add(uid)
+            ent = entries.get(uid)
+            if ent is None:
+                out.append(ev)
+            elif ent[0] != ev[E_RV]:
+                out.append((MODIFIED,) + ev[1:])
+        for uid, ent in list(entries.items()):
+            if uid in seen or (scope_ns is not None and ent[NS] != scope_ns):
+                continue
+            core = ent[CORE]
+            if core is None:
+                core = self.decoder.core_from_summary(uid, ent[NS], ent[NAME], ent[PHASE])
+            out.append((DELETED, uid, ent[NS], ent[NAME], ent[0], ent[PHASE], True, None, core))
+        if not notify:
+            for ev in out:
+                uid = ev[E_UID]
+                if ev[E_TYPE] == DELETED:
+                    entries.pop(uid, None)
+                else:
+                    entries[uid] = [ev[E_RV], ev[E_PHASE], ev[E_NS], ev[E_NAME], None]
+            return []
+        saved_rv = self.last_rv
+        ctrl = self.handle_batch(out, read_ns)
+        self.last_rv = saved_rv  # the list RV, set by the caller, stays authoritative
+        return ctrl

@@ -1,0 +1,232 @@
+"""List-then-watch reflector with resume, bookmarks and 410 recovery.
+
+Reference: ``self.watch.stream(self.v1.list_pod_for_all_namespaces)``
+(``/root/reference/watcher/pod_watcher.py:264``). The library re-issues the
+watch from the last seen resourceVersion when the server closes it, gives up
+when it never saw one, and raises on the second 410 so the process exits and
+Kubernetes restarts it, replaying every pod as ``ADDED``.
+
+This reflector:
+
+* LISTs (paginated, ``watcher.list_page_size``) and diffs the result against
+  the pod cache (:meth:`EventPipeline.reconcile`) — on first start this turns
+  every existing pod into ``ADDED``, the same thing the reference's watch
+  without a resourceVersion produces;
+* WATCHes from the list/last resourceVersion with ``allowWatchBookmarks`` and
+  a server-side ``timeoutSeconds``; a normal server close resumes from the last
+  resourceVersion with no relist;
+* on ``410 Gone`` (HTTP status or ``ERROR`` event) relists and reconciles, so
+  no state change is lost and unchanged pods are not re-notified;
+* on transport errors backs off per ``watcher.retry`` and gives up after
+  ``max_attempts`` consecutive failures (0 = never), raising
+  :class:`WatchFailed`;
+* pauses its socket while the notifier reports backpressure.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import logging
+import time
+from typing import Optional
+
+from ..kube.api import ApiError, KubeApi
+from ..metrics import Metrics
+from ..net.http import HttpError
+from ..ops.decode import E_EXTRA, E_TYPE, ERROR, INVALID
+from ..utils.backoff import Backoff
+from ..utils.config import Settings
+from ..utils.logsetup import SERVICE_LOGGER
+from .pipeline import EventPipeline
+
+
+class Expired(Exception):
+    """The watch resourceVersion is too old (410 Gone)."""
+
+
+class WatchFailed(Exception):
+    """Consecutive watch failures exhausted ``watcher.retry.max_attempts``."""
+
+
+class Reflector:
+    def __init__(self, api: KubeApi, settings: Settings, decoder, pipeline: EventPipeline,
+                 metrics: Metrics, namespace: Optional[str] = None,
+                 resource_version: Optional[str] = None, primed: bool = False) -> None:
+        self.api = api
+        self.settings = settings
+        self.decoder = decoder
+        self.pipeline = pipeline
+        self.metrics = metrics
+        self.namespace = namespace
+        self.rv = resource_version
+        self.primed = primed
+        self.log = logging.getLogger(SERVICE_LOGGER)
+        self.stream = None
+        self._paused = False
+        self._stop = asyncio.Event()
+        self.connected = asyncio.Event()
+        self.synced = asyncio.Event()
+        self.watch_count = 0
+
+    @property
+    def scope(self) -> str:
+        return self.namespace or "*"
+
+    # ------------------------------------------------------------------ control
+    def stop(self) -> None:
+        self._stop.set()
+        if self.stream is not None:
+            self.stream.close()
+
+    def set_paused(self, paused: bool) -> None:
+        self._paused = paused
+        s = self.stream
+        if s is not None and s._proto.transport is not None:
+            if paused:
+                s._proto.transport.pause_reading()
+            else:
+                s._proto.transport.resume_reading()
+
+    # ------------------------------------------------------------------ list
+    async def relist(self, notify: bool = True) -> None:
+        w = self.settings.watcher
+        events = []
+        cont = None
+        list_rv = None
+        while True:
+            body = await self.api.list_pods_raw(
+                namespace=self.namespace, limit=w.list_page_size, continue_token=cont,
+                label_selector=w.label_selector, field_selector=w.field_selector)
+            page_rv, cont, evs = self.decoder.decode_list(body)
+            if list_rv is None:
+                list_rv = page_rv
+            events.extend(evs)
+            if not cont:
+                break
+        self.metrics.c["relists"] += 1
+        read_ns = time.monotonic_ns()
+        ctrl = self.pipeline.reconcile(events, read_ns, notify=notify,
+                                       scope_ns=self.namespace if self._scoped() else None)
+        for ev in ctrl:
+            self._handle_control(ev)
+        self.rv = list_rv
+        self.pipeline.last_rv = list_rv
+        self.synced.set()
+
+    def _scoped(self) -> bool:
+        return self.namespace is not None
+
+    # ------------------------------------------------------------------ watch
+    def _handle_control(self, ev: tuple) -> None:
+        if ev[E_TYPE] == INVALID:
+            self.metrics.c["events_invalid"] += 1
+            self.log.warning(f"Skipping undecodable watch line: {ev[E_EXTRA]}")
+            return
+        status = ev[E_EXTRA] or {}
+        code = status.get("code")
+        if code == 410 or status.get("reason") in ("Expired", "Gone"):
+            self._expired = True
+        else:
+            self.log.warning(f"Watch ERROR event: {status.get('message') or status}")
+            self._error = True
+        if self.stream is not None:
+            self.stream.close()
+
+    async def watch_once(self) -> None:
+        w = self.settings.watcher
+        self.decoder.reset()
+        self._expired = False
+        self._error = False
+        pipeline = self.pipeline
+        decoder = self.decoder
+
+        def sink(data: bytes, read_ns: int) -> None:
+            evs = decoder.feed(data)
+            if evs:
+                ctrl = pipeline.handle_batch(evs, read_ns)
+                if pipeline.last_rv:
+                    self.rv = pipeline.last_rv
+                for ev in ctrl:
+                    self._handle_control(ev)
+
+        pipeline.last_rv = self.rv
+        self.stream = await self.api.watch_pods(
+            sink, namespace=self.namespace, resource_version=self.rv,
+            timeout_seconds=w.watch_timeout_seconds or None, allow_bookmarks=True,
+            label_selector=w.label_selector, field_selector=w.field_selector)
+        self.watch_count += 1
+        self.connected.set()
+        if self._stop.is_set():
+            self.stream.close()
+        if self._paused:
+            self.set_paused(True)
+        idle_limit = (w.watch_timeout_seconds or 300) + 60
+        try:
+            finished = self.stream.finished
+            while not finished.done():
+                # asyncio.wait (not wait_for): never swallows a cancellation on 3.10
+                await asyncio.wait([finished], timeout=5.0)
+                if (not finished.done() and not self._paused
+                        and time.monotonic() - self.stream.last_activity > idle_limit):
+                    self.log.warning("Watch stream idle for too long; reconnecting")
+                    self.stream.close()
+        finally:
+            self.stream.close()
+            self.stream = None
+        if self._expired:
+            raise Expired()
+        if self._error:
+            raise HttpError("watch ended with an ERROR event")
+
+    async def run(self) -> None:
+        w = self.settings.watcher
+        backoff = Backoff(w.retry)
+        need_list = self.rv is None
+        first = not self.primed
+        failures = 0
+        while not self._stop.is_set():
+            try:
+                if need_list:
+                    notify = not (first and w.initial_list == "skip")
+                    await self.relist(notify=notify)
+                    need_list = False
+                    first = False
+                else:
+                    self.synced.set()
+                await self.watch_once()
+                failures = 0
+                backoff.reset()
+                if not self._stop.is_set():
+                    self.metrics.c["watch_restarts"] += 1
+            except Expired:
+                self.metrics.c["expired_410"] += 1
+                self.log.warning(f"Watch resourceVersion {self.rv} expired (410); relisting")
+                need_list = True
+                failures = 0
+            except ApiError as exc:
+                if exc.status == 410:
+                    self.metrics.c["expired_410"] += 1
+                    self.log.warning(f"Watch resourceVersion {self.rv} expired (410); relisting")
+                    need_list = True
+                    continue
+                failures += 1
+                await self._backoff(backoff, failures, exc)
+            except HttpError as exc:
+                if self._stop.is_set():
+                    break
+                failures += 1
+                await self._backoff(backoff, failures, exc)
+
+    async def _backoff(self, backoff: Backoff, failures: int, exc: Exception) -> None:
+        limit = self.settings.watcher.retry.max_attempts
+        if limit and failures >= limit:
+            self.log.error(f"Error in Pod watcher: {exc}")
+            raise WatchFailed(str(exc)) from exc
+        delay = backoff.next_delay()
+        self.log.warning(f"Watch failed ({exc}); retry {failures}/{limit or 'inf'} in {delay:.2f}s")
+        self.metrics.c["watch_restarts"] += 1
+        waiter = asyncio.ensure_future(self._stop.wait())
+        try:
+            await asyncio.wait([waiter], timeout=delay)
+        finally:
+            waiter.cancel()

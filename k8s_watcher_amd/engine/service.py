@@ -1,0 +1,276 @@
+"""Watcher service orchestrator (SURVEY C6 + C7, layer L4).
+
+Reference: ``PodWatcher.setup_k8s_client`` + ``start_watching``
+(``/root/reference/watcher/pod_watcher.py:110-157,243-277``). The same log
+messages (§2.4) are emitted in the same order; the behavioural fixes are:
+
+* the connectivity probe is ``GET /version`` (``CoreV1Api.get_api_version``
+  at ``:140`` does not exist and makes the reference fail setup);
+* the namespace sample is bounded (``limit=5``) instead of listing them all;
+* setup failure is an error the CLI turns into exit status 1 (the reference
+  returns and exits 0, ``:245-247``);
+* the clusterapi notifier is enabled and health-checked (``:14,236,250-253``
+  are commented out in the reference);
+* SIGTERM and SIGINT both stop the watch, drain the notifier and write a
+  final checkpoint.
+
+With ``watcher.namespace_scope: server`` one reflector per target namespace
+watches ``/api/v1/namespaces/<ns>/pods``, so the API server only sends the
+pods the watcher cares about (the reference always watches the whole cluster
+and filters client-side).
+"""
+
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import time
+from typing import List, Optional
+
+from ..kube.api import ApiError, KubeApi
+from ..kube.kubeconfig import ConfigException, KubeEndpoint, load_incluster_config, load_kube_config
+from ..metrics import Metrics, start_metrics_server
+from ..net.http import HttpError
+from ..ops.cache import PodCache
+from ..ops.decode import make_decoder
+from ..parallel.notifier import NotifierPool, NullNotifier
+from ..utils.config import Settings
+from ..utils.logsetup import SERVICE_LOGGER
+from .checkpoint import load_checkpoint, save_checkpoint
+from .pipeline import EventPipeline
+from .reflector import Reflector, WatchFailed
+
+
+class SetupError(Exception):
+    """The Kubernetes client could not be set up (reference ``:246``)."""
+
+
+class WatcherService:
+    def __init__(self, settings: Settings, endpoint: Optional[KubeEndpoint] = None,
+                 metrics: Optional[Metrics] = None, notifier_factory=None) -> None:
+        self.settings = settings
+        self.endpoint = endpoint
+        self.metrics = metrics or Metrics()
+        self.notifier_factory = notifier_factory
+        self.log = logging.getLogger(SERVICE_LOGGER)
+        self.api: Optional[KubeApi] = None
+        self.notifier = None
+        self.pipeline: Optional[EventPipeline] = None
+        self.reflectors: List[Reflector] = []
+        self.decoder = None
+        self._stop = asyncio.Event()
+        self._tasks: List[asyncio.Task] = []
+        self._metrics_server = None
+        self.started = asyncio.Event()
+        self.server_version: Optional[str] = None
+
+    # ------------------------------------------------------------------ setup
+    def load_endpoint(self) -> KubeEndpoint:
+        k = self.settings.kubernetes
+        if self.endpoint is not None:
+            return self.endpoint
+        if k.use_incluster_config:
+            self.log.info("Using in-cluster configuration")
+            return load_incluster_config()
+        if k.config_file:
+            self.log.info(f"Loading kubeconfig from: {k.config_file}")
+            if not os.path.exists(k.config_file):
+                self.log.error(f"Kubeconfig file not found: {k.config_file}")
+                raise SetupError(f"kubeconfig not found: {k.config_file}")
+            return load_kube_config(config_file=k.config_file, context=k.context)
+        self.log.info("Using default kubeconfig")
+        return load_kube_config(context=k.context)
+
+    async def setup_k8s_client(self) -> bool:
+        """Reference-compatible setup: returns False (after logging) on failure."""
+        try:
+            ep = self.load_endpoint()
+            self.endpoint = ep
+            self.api = KubeApi(ep, timeout=self.settings.kubernetes.request_timeout)
+            ver = await self.api.get_version()
+            self.server_version = ver.get("gitVersion") or f"{ver.get('major')}.{ver.get('minor')}"
+            self.log.info(f"Successfully connected to Kubernetes API version: {self.server_version}")
+            try:
+                nss = await self.api.list_namespaces(limit=5)
+                names = [(i.get("metadata") or {}).get("name") for i in (nss.get("items") or [])[:5]]
+                self.log.info(f"Sample namespaces: {names}")
+            except ApiError as exc:
+                # RBAC may not grant namespace list; the watch itself only needs pods.
+                self.log.warning(f"Could not list namespaces: {exc}")
+            return True
+        except ConfigException as exc:
+            self.log.error(f"Kubernetes config error: {exc}")
+        except SetupError:
+            pass
+        except (ApiError, HttpError, OSError, ValueError) as exc:
+            self.log.error(f"Error setting up k8s client: {exc}")
+        if self.api is not None:
+            await self.api.close()
+            self.api = None
+        return False
+
+    def _make_notifier(self):
+        c = self.settings.clusterapi
+        w = self.settings.watcher
+        if self.notifier_factory is not None:
+            return self.notifier_factory(self)
+        if not c.enabled:
+            return NullNotifier(self.metrics)
+        log_events = w.log_events if w.log_events is not None else self.log.isEnabledFor(logging.INFO)
+        return NotifierPool(c, self.metrics, ts_mode=w.event_timestamp, log_events=log_events,
+                            on_saturation=self._on_saturation)
+
+    def _on_saturation(self, saturated: bool) -> None:
+        for r in self.reflectors:
+            r.set_paused(saturated)
+
+    # ------------------------------------------------------------------ run
+    async def start(self) -> None:
+        """Setup + start background tasks; returns once every scope has synced."""
+        s = self.settings
+        if not await self.setup_k8s_client():
+            self.log.error("Failed to setup Kubernetes client")
+            raise SetupError("Failed to setup Kubernetes client")
+        assert self.api is not None
+        self.notifier = self._make_notifier()
+        if s.clusterapi.enabled and s.clusterapi.health_check_on_start:
+            if await self.notifier.health_check():
+                self.log.info("ClusterAPI health check passed")
+            else:
+                self.log.warning("ClusterAPI health check failed, but continuing...")
+        self.decoder = make_decoder(s.watcher.engine, s.environment, s.watcher.state_format)
+        scopes = (list(s.watcher.namespaces)
+                  if s.watcher.namespace_scope == "server" and s.watcher.namespaces else [None])
+        cache = PodCache()
+        saved_rvs = {}
+        ck = s.watcher.checkpoint.path
+        if ck:
+            loaded = load_checkpoint(ck)
+            if loaded is not None:
+                saved_rvs, cache, _ = loaded
+                self.log.info(f"Resuming from checkpoint {ck}: {len(cache)} cached pods")
+        self.pipeline = EventPipeline(s, self.decoder, self.notifier, self.metrics, cache)
+        self.metrics.gauges["cached_pods"] = lambda: float(len(cache))
+        self.metrics.gauges["notify_outstanding"] = lambda: float(self.notifier.outstanding())
+        self.log.info(f"Starting Pod watcher in {s.environment} environment...")
+        if s.watcher.namespaces:
+            self.log.info(f"Monitoring namespaces: {s.watcher.namespaces}")
+        else:
+            self.log.info("Monitoring all namespaces")
+        for ns in scopes:
+            key = ns or "*"
+            rv = saved_rvs.get(key)
+            # Each scope decodes its own stream: give it a private decoder.
+            dec = self.decoder if len(scopes) == 1 else make_decoder(
+                s.watcher.engine, s.environment, s.watcher.state_format)
+            pipe = self.pipeline if len(scopes) == 1 else self._scope_pipeline(dec)
+            self.reflectors.append(Reflector(self.api, s, dec, pipe, self.metrics, namespace=ns,
+                                             resource_version=rv, primed=bool(saved_rvs)))
+        for r in self.reflectors:
+            self._tasks.append(asyncio.ensure_future(r.run()))
+        if s.metrics.enabled:
+            self._metrics_server = await start_metrics_server(self.metrics, s.metrics.host, s.metrics.port)
+        if ck:
+            self._tasks.append(asyncio.ensure_future(self._checkpoint_loop()))
+        await self._wait_synced()
+        self.metrics.ready = True
+        self.started.set()
+
+    def _scope_pipeline(self, decoder) -> EventPipeline:
+        assert self.pipeline is not None
+        p = EventPipeline(self.settings, decoder, self.notifier, self.metrics, self.pipeline.cache)
+        return p
+
+    async def _wait_synced(self) -> None:
+        synced = asyncio.ensure_future(asyncio.gather(*[r.synced.wait() for r in self.reflectors]))
+        runs = list(self._tasks)
+        done, _ = await asyncio.wait([synced] + runs, return_when=asyncio.FIRST_COMPLETED)
+        if synced not in done:
+            synced.cancel()
+            for t in runs:
+                if t.done() and t.exception() is not None:
+                    raise t.exception()  # type: ignore[misc]
+            raise SetupError("watch ended before the initial sync")
+
+    async def wait(self) -> None:
+        """Run until :meth:`stop` or a reflector fails permanently."""
+        stopper = asyncio.ensure_future(self._stop.wait())
+        tasks = [t for t in self._tasks] + [stopper]
+        done, _ = await asyncio.wait(tasks, return_when=asyncio.FIRST_COMPLETED)
+        err = None
+        for t in done:
+            if t is not stopper and t.exception() is not None:
+                err = t.exception()
+        if not stopper.done():
+            stopper.cancel()
+        if err is not None:
+            raise err
+
+    def stop(self) -> None:
+        self._stop.set()
+        for r in self.reflectors:
+            r.stop()
+
+    async def shutdown(self, drain_timeout: float = 10.0) -> None:
+        self.log.info("Stopping Pod watcher...")
+        for r in self.reflectors:
+            r.stop()
+        if self.notifier is not None:
+            await self.notifier.drain(drain_timeout)
+        await self._write_checkpoint()
+        for t in self._tasks:
+            if not t.done():
+                t.cancel()
+        for t in self._tasks:
+            try:
+                await t
+            except (asyncio.CancelledError, WatchFailed, Exception):  # noqa: BLE001
+                pass
+        if self._metrics_server is not None:
+            self._metrics_server.close()
+        if self.notifier is not None:
+            await self.notifier.close()
+        if self.api is not None:
+            await self.api.close()
+
+    async def run(self) -> None:
+        try:
+            await self.start()
+            await self.wait()
+        finally:
+            await self.shutdown()
+
+    # ------------------------------------------------------------------ checkpoint
+    async def _write_checkpoint(self) -> None:
+        ck = self.settings.watcher.checkpoint.path
+        if not ck or self.pipeline is None:
+            return
+        scopes = {r.scope: r.rv for r in self.reflectors}
+        save_checkpoint(ck, scopes, self.pipeline.cache, {"written_at": time.time()})
+        self.metrics.c["checkpoints_written"] += 1
+
+    async def checkpoint_now(self, drain_timeout: float = 30.0) -> bool:
+        """Quiescent checkpoint: pause readers, drain notifier, save, resume."""
+        for r in self.reflectors:
+            r.set_paused(True)
+        try:
+            ok = await self.notifier.drain(drain_timeout) if self.notifier is not None else True
+            if ok:
+                await self._write_checkpoint()
+            return ok
+        finally:
+            saturated = getattr(self.notifier, "saturated", False)
+            for r in self.reflectors:
+                r.set_paused(saturated)
+
+    async def _checkpoint_loop(self) -> None:
+        period = self.settings.watcher.checkpoint.interval_seconds
+        last = None
+        while True:
+            await asyncio.sleep(period)
+            state = (tuple(r.rv for r in self.reflectors), len(self.pipeline.cache) if self.pipeline else 0)
+            if state == last:
+                continue
+            if await self.checkpoint_now():
+                last = state

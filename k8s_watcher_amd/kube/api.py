@@ -1,0 +1,121 @@
+"""Async subset of the Kubernetes core/v1 REST API that a pod watcher needs.
+
+Replaces the ``kubernetes`` library calls the reference makes
+(``/root/reference/watcher/pod_watcher.py:137-146,264``;
+``test_k8s_connection.py:32-48``): ``GET /version``, ``GET /api/v1/namespaces``,
+paginated ``GET /api/v1/pods`` (or ``/api/v1/namespaces/{ns}/pods``) and the
+streaming watch on the same paths. Bodies are returned as raw bytes so the
+event decoder (native or Python) is the only place JSON is parsed.
+"""
+
+from __future__ import annotations
+
+import json
+from typing import Callable, Dict, Optional, Tuple
+
+from ..net.http import HttpClient, HttpError, Response, StreamResponse
+from .kubeconfig import KubeEndpoint
+
+USER_AGENT = "k8s-watcher-amd/1.0"
+
+
+class ApiError(Exception):
+    """Non-2xx answer from the API server (``status`` = HTTP code)."""
+
+    def __init__(self, status: int, reason: str, body: bytes) -> None:
+        self.status = status
+        self.reason = reason
+        self.body = body
+        msg = reason
+        try:
+            doc = json.loads(body)
+            msg = doc.get("message") or reason
+            self.k8s_reason = doc.get("reason")
+        except (ValueError, AttributeError):
+            self.k8s_reason = None
+        super().__init__(f"({status}) {msg}")
+
+
+def pods_path(namespace: Optional[str] = None) -> str:
+    return f"/api/v1/namespaces/{namespace}/pods" if namespace else "/api/v1/pods"
+
+
+class KubeApi:
+    def __init__(self, endpoint: KubeEndpoint, timeout: float = 30.0) -> None:
+        self.endpoint = endpoint
+        headers = {"Accept": "application/json", "User-Agent": USER_AGENT}
+        headers.update(endpoint.static_headers)
+        self.http = HttpClient(endpoint.server, endpoint.ssl_context, headers=headers,
+                               timeout=timeout, header_provider=endpoint.header_provider)
+
+    async def _get(self, path: str, query: Optional[Dict[str, object]] = None,
+                   timeout: Optional[float] = None) -> Response:
+        resp = await self.http.request("GET", path, query=query, timeout=timeout)
+        if not resp.ok:
+            raise ApiError(resp.status, resp.reason, resp.body)
+        return resp
+
+    async def get_version(self) -> Dict[str, object]:
+        """``GET /version`` — the connectivity probe the reference meant to run."""
+        return (await self._get("/version")).json()
+
+    async def list_namespaces(self, limit: Optional[int] = None, continue_token: Optional[str] = None) -> Dict:
+        q: Dict[str, object] = {}
+        if limit:
+            q["limit"] = limit
+        if continue_token:
+            q["continue"] = continue_token
+        return (await self._get("/api/v1/namespaces", q)).json()
+
+    async def list_pods_raw(self, namespace: Optional[str] = None, limit: Optional[int] = None,
+                            continue_token: Optional[str] = None, label_selector: Optional[str] = None,
+                            field_selector: Optional[str] = None,
+                            resource_version: Optional[str] = None,
+                            timeout: Optional[float] = None) -> bytes:
+        q: Dict[str, object] = {}
+        if limit:
+            q["limit"] = limit
+        if continue_token:
+            q["continue"] = continue_token
+        if label_selector:
+            q["labelSelector"] = label_selector
+        if field_selector:
+            q["fieldSelector"] = field_selector
+        if resource_version is not None:
+            q["resourceVersion"] = resource_version
+        return (await self._get(pods_path(namespace), q, timeout)).body
+
+    async def watch_pods(self, sink: Callable[[bytes, int], None], namespace: Optional[str] = None,
+                         resource_version: Optional[str] = None, timeout_seconds: Optional[int] = None,
+                         allow_bookmarks: bool = True, label_selector: Optional[str] = None,
+                         field_selector: Optional[str] = None,
+                         connect_timeout: Optional[float] = None) -> StreamResponse:
+        """Open ``?watch=true``; de-chunked body bytes go to ``sink(data, read_ns)``."""
+        q: Dict[str, object] = {"watch": "true"}
+        if resource_version:
+            q["resourceVersion"] = resource_version
+        if allow_bookmarks:
+            q["allowWatchBookmarks"] = "true"
+        if timeout_seconds:
+            q["timeoutSeconds"] = int(timeout_seconds)
+        if label_selector:
+            q["labelSelector"] = label_selector
+        if field_selector:
+            q["fieldSelector"] = field_selector
+        stream, err = await self.http.stream("GET", pods_path(namespace), sink, query=q,
+                                             timeout=connect_timeout)
+        if err is not None:
+            raise ApiError(stream.status, stream.reason, err)
+        return stream
+
+    async def close(self) -> None:
+        await self.http.close()
+
+
+def split_list_body(body: bytes) -> Tuple[Dict, list]:
+    """Parse a ``*List`` body into ``(metadata, items)`` with the stdlib decoder."""
+    doc = json.loads(body)
+    return doc.get("metadata") or {}, doc.get("items") or []
+
+
+__all__ = ["ApiError", "HttpError", "KubeApi", "pods_path", "split_list_body"]

@@ -1,0 +1,340 @@
+"""Kubeconfig and in-cluster credential loading.
+
+The reference calls ``kubernetes.config.load_incluster_config()`` /
+``load_kube_config(config_file=...)`` / ``load_kube_config()``
+(``/root/reference/watcher/pod_watcher.py:115-134``). That library is not
+available, so this module implements the subset of its behaviour a pod
+watcher needs, returning a :class:`KubeEndpoint` (server URL, TLS context,
+auth-header provider) instead of mutating a global ``Configuration``.
+
+Kubeconfig support: ``current-context`` or an explicit context; ``$KUBECONFIG``
+(``:``-separated, first definition of a name wins) then ``~/.kube/config``;
+``server``, ``certificate-authority[-data]``, ``insecure-skip-tls-verify``,
+``tls-server-name``; user ``token`` / ``tokenFile`` / basic auth /
+``client-certificate[-data]`` + ``client-key[-data]`` / ``exec`` credential
+plugins. Relative file paths resolve against the kubeconfig's directory.
+
+In-cluster: ``$KUBERNETES_SERVICE_HOST``/``$KUBERNETES_SERVICE_PORT`` and the
+service-account token + CA; the token file is re-read periodically so bound
+(rotating) tokens keep working — something the reference's one-shot load
+does not do.
+"""
+
+from __future__ import annotations
+
+import base64
+import json
+import os
+import ssl
+import subprocess
+import tempfile
+import time
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+import yaml
+
+SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
+class ConfigException(Exception):
+    """Same role as ``kubernetes.config.ConfigException`` (``pod_watcher.py:2,152``)."""
+
+
+@dataclass
+class KubeEndpoint:
+    server: str
+    ssl_context: Optional[ssl.SSLContext] = None
+    static_headers: Dict[str, str] = field(default_factory=dict)
+    header_provider: Optional[Callable[[], Dict[str, str]]] = None
+    namespace: Optional[str] = None
+    source: str = ""
+    context_name: Optional[str] = None
+
+    def auth_headers(self) -> Dict[str, str]:
+        h = dict(self.static_headers)
+        if self.header_provider is not None:
+            h.update(self.header_provider())
+        return h
+
+
+# --------------------------------------------------------------------------- helpers
+
+
+def _read_yaml(path: str) -> Dict[str, Any]:
+    try:
+        with open(path, "r", encoding="utf-8") as fh:
+            data = yaml.safe_load(fh) or {}
+    except FileNotFoundError:
+        raise ConfigException(f"Invalid kube-config file. No configuration found: {path}") from None
+    except yaml.YAMLError as exc:
+        raise ConfigException(f"Invalid kube-config file {path}: {exc}") from None
+    if not isinstance(data, dict):
+        raise ConfigException(f"Invalid kube-config file {path}: not a mapping")
+    return data
+
+
+def kubeconfig_paths(config_file: Optional[str] = None) -> List[str]:
+    if config_file:
+        return [os.path.expanduser(config_file)]
+    env = os.environ.get("KUBECONFIG")
+    if env:
+        return [os.path.expanduser(p) for p in env.split(os.pathsep) if p]
+    return [os.path.expanduser("~/.kube/config")]
+
+
+def _named(items: Optional[List[Dict[str, Any]]], key: str) -> Dict[str, Tuple[Dict[str, Any], str]]:
+    out: Dict[str, Tuple[Dict[str, Any], str]] = {}
+    for it in items or []:
+        if isinstance(it, dict) and "name" in it:
+            out[it["name"]] = (it.get(key) or {}, "")
+    return out
+
+
+class KubeConfigDocument:
+    """The merged view of one or more kubeconfig files."""
+
+    def __init__(self, paths: List[str]) -> None:
+        self.paths = paths
+        self.clusters: Dict[str, Tuple[Dict[str, Any], str]] = {}
+        self.users: Dict[str, Tuple[Dict[str, Any], str]] = {}
+        self.contexts: Dict[str, Tuple[Dict[str, Any], str]] = {}
+        self.context_order: List[str] = []
+        self.current_context: Optional[str] = None
+        found = False
+        for p in paths:
+            if not os.path.exists(p):
+                continue
+            found = True
+            doc = _read_yaml(p)
+            base = os.path.dirname(os.path.abspath(p))
+            for section, key, store in (("clusters", "cluster", self.clusters),
+                                        ("users", "user", self.users),
+                                        ("contexts", "context", self.contexts)):
+                for name, (body, _) in _named(doc.get(section), key).items():
+                    if name not in store:
+                        store[name] = (body, base)
+                        if section == "contexts":
+                            self.context_order.append(name)
+            if self.current_context is None and doc.get("current-context"):
+                self.current_context = doc["current-context"]
+        if not found:
+            raise ConfigException(f"Invalid kube-config file. No configuration found: {':'.join(paths)}")
+
+    def list_contexts(self) -> Tuple[List[Dict[str, Any]], Optional[Dict[str, Any]]]:
+        ctxs = [{"name": n, "context": dict(self.contexts[n][0])} for n in self.context_order]
+        active = next((c for c in ctxs if c["name"] == self.current_context), None)
+        return ctxs, active
+
+
+def _resolve(base: str, path: Optional[str]) -> Optional[str]:
+    if not path:
+        return None
+    path = os.path.expanduser(path)
+    return path if os.path.isabs(path) else os.path.join(base, path)
+
+
+def _b64(data: str) -> bytes:
+    return base64.b64decode(data.encode("ascii") if isinstance(data, str) else data)
+
+
+def _load_cert_chain(ctx: ssl.SSLContext, cert_pem: bytes, key_pem: bytes) -> None:
+    # ssl only loads client certs from files: stage them in private temp files.
+    fds = []
+    try:
+        paths = []
+        for blob in (cert_pem, key_pem):
+            fd, p = tempfile.mkstemp(prefix="kw-", suffix=".pem")
+            os.fchmod(fd, 0o600)
+            with os.fdopen(fd, "wb") as fh:
+                fh.write(blob)
+            paths.append(p)
+            fds.append(p)
+        ctx.load_cert_chain(paths[0], paths[1])
+    finally:
+        for p in fds:
+            try:
+                os.unlink(p)
+            except OSError:
+                pass
+
+
+def build_ssl_context(ca_file: Optional[str] = None, ca_data: Optional[bytes] = None,
+                      insecure: bool = False, cert_pem: Optional[bytes] = None,
+                      key_pem: Optional[bytes] = None, server_name: Optional[str] = None) -> ssl.SSLContext:
+    if insecure:
+        ctx = ssl.create_default_context()
+        ctx.check_hostname = False
+        ctx.verify_mode = ssl.CERT_NONE
+    elif ca_file or ca_data:
+        ctx = ssl.create_default_context(cafile=ca_file,
+                                         cadata=ca_data.decode("ascii") if ca_data else None)
+    else:
+        ctx = ssl.create_default_context()
+    if cert_pem and key_pem:
+        _load_cert_chain(ctx, cert_pem, key_pem)
+    if server_name:
+        ctx.check_hostname = False  # hostname checked against tls-server-name is not expressible; trust the CA
+    return ctx
+
+
+class _ExecCredential:
+    """Runs a client-go ``exec`` credential plugin and caches its token."""
+
+    def __init__(self, spec: Dict[str, Any]) -> None:
+        self.spec = spec
+        self._token: Optional[str] = None
+        self._expiry: float = 0.0
+
+    def headers(self) -> Dict[str, str]:
+        now = time.time()
+        if self._token is None or (self._expiry and now >= self._expiry - 10):
+            self._refresh()
+        return {"Authorization": f"Bearer {self._token}"} if self._token else {}
+
+    def _refresh(self) -> None:
+        cmd = [self.spec.get("command")] + list(self.spec.get("args") or [])
+        if not cmd[0]:
+            raise ConfigException("exec credential plugin has no command")
+        env = dict(os.environ)
+        for item in self.spec.get("env") or []:
+            env[item["name"]] = item["value"]
+        api_version = self.spec.get("apiVersion", "client.authentication.k8s.io/v1beta1")
+        env["KUBERNETES_EXEC_INFO"] = json.dumps(
+            {"apiVersion": api_version, "kind": "ExecCredential", "spec": {"interactive": False}})
+        try:
+            out = subprocess.run(cmd, env=env, capture_output=True, check=True, timeout=60).stdout
+        except (OSError, subprocess.SubprocessError) as exc:
+            raise ConfigException(f"exec credential plugin {cmd[0]!r} failed: {exc}") from None
+        try:
+            status = json.loads(out).get("status") or {}
+        except ValueError:
+            raise ConfigException("exec credential plugin returned invalid JSON") from None
+        self._token = status.get("token")
+        exp = status.get("expirationTimestamp")
+        self._expiry = 0.0
+        if exp:
+            from ..utils.timefmt import parse_k8s_time
+            dt = parse_k8s_time(exp)
+            if dt is not None:
+                self._expiry = dt.timestamp()
+
+
+class _TokenFile:
+    """Bearer token read from a file and re-read every ``period`` seconds."""
+
+    def __init__(self, path: str, period: float = 60.0) -> None:
+        self.path = path
+        self.period = period
+        self._token = ""
+        self._read_at = 0.0
+        self._read()
+
+    def _read(self) -> None:
+        try:
+            with open(self.path, "r", encoding="utf-8") as fh:
+                self._token = fh.read().strip()
+        except OSError as exc:
+            if not self._token:
+                raise ConfigException(f"cannot read token file {self.path}: {exc}") from None
+        self._read_at = time.monotonic()
+
+    def headers(self) -> Dict[str, str]:
+        if time.monotonic() - self._read_at > self.period:
+            self._read()
+        return {"Authorization": f"Bearer {self._token}"} if self._token else {}
+
+
+# --------------------------------------------------------------------------- loaders
+
+
+def list_kube_config_contexts(config_file: Optional[str] = None):
+    """``(contexts, active_context)`` like ``kubernetes.config.list_kube_config_contexts``."""
+    return KubeConfigDocument(kubeconfig_paths(config_file)).list_contexts()
+
+
+def load_kube_config(config_file: Optional[str] = None, context: Optional[str] = None) -> KubeEndpoint:
+    paths = kubeconfig_paths(config_file)
+    doc = KubeConfigDocument(paths)
+    ctx_name = context or doc.current_context
+    if not ctx_name:
+        raise ConfigException("Invalid kube-config file. Expected key current-context")
+    if ctx_name not in doc.contexts:
+        raise ConfigException(f"Invalid kube-config file. Expected object with name {ctx_name} in contexts list")
+    ctx, _ = doc.contexts[ctx_name]
+    cluster_name = ctx.get("cluster")
+    if cluster_name not in doc.clusters:
+        raise ConfigException(f"Invalid kube-config file. Expected object with name {cluster_name} in clusters list")
+    cluster, cbase = doc.clusters[cluster_name]
+    user, ubase = doc.users.get(ctx.get("user"), ({}, os.getcwd()))
+    server = cluster.get("server")
+    if not server:
+        raise ConfigException(f"cluster {cluster_name!r} has no server")
+
+    headers: Dict[str, str] = {}
+    provider: Optional[Callable[[], Dict[str, str]]] = None
+    if user.get("token"):
+        headers["Authorization"] = f"Bearer {user['token']}"
+    elif user.get("tokenFile"):
+        provider = _TokenFile(_resolve(ubase, user["tokenFile"])).headers  # type: ignore[arg-type]
+    elif user.get("exec"):
+        provider = _ExecCredential(user["exec"]).headers
+    elif user.get("username") and user.get("password"):
+        cred = base64.b64encode(f"{user['username']}:{user['password']}".encode()).decode()
+        headers["Authorization"] = f"Basic {cred}"
+
+    ssl_ctx = None
+    if server.startswith("https://"):
+        ca_data = _b64(cluster["certificate-authority-data"]) if cluster.get("certificate-authority-data") else None
+        cert = key = None
+        if user.get("client-certificate-data"):
+            cert = _b64(user["client-certificate-data"])
+        elif user.get("client-certificate"):
+            with open(_resolve(ubase, user["client-certificate"]), "rb") as fh:  # type: ignore[arg-type]
+                cert = fh.read()
+        if user.get("client-key-data"):
+            key = _b64(user["client-key-data"])
+        elif user.get("client-key"):
+            with open(_resolve(ubase, user["client-key"]), "rb") as fh:  # type: ignore[arg-type]
+                key = fh.read()
+        try:
+            ssl_ctx = build_ssl_context(
+                ca_file=_resolve(cbase, cluster.get("certificate-authority")),
+                ca_data=ca_data,
+                insecure=bool(cluster.get("insecure-skip-tls-verify")),
+                cert_pem=cert, key_pem=key,
+                server_name=cluster.get("tls-server-name"))
+        except (ssl.SSLError, OSError, ValueError) as exc:
+            raise ConfigException(f"TLS setup for cluster {cluster_name!r} failed: {exc}") from None
+    return KubeEndpoint(server=server.rstrip("/"), ssl_context=ssl_ctx, static_headers=headers,
+                        header_provider=provider, namespace=ctx.get("namespace"),
+                        source=":".join(paths), context_name=ctx_name)
+
+
+def load_incluster_config(sa_dir: str = SA_DIR, environ: Optional[Dict[str, str]] = None,
+                          token_refresh_seconds: float = 60.0) -> KubeEndpoint:
+    env = os.environ if environ is None else environ
+    host = env.get("KUBERNETES_SERVICE_HOST")
+    port = env.get("KUBERNETES_SERVICE_PORT")
+    if not host or not port:
+        raise ConfigException("Service host/port is not set.")
+    token_path = os.path.join(sa_dir, "token")
+    ca_path = os.path.join(sa_dir, "ca.crt")
+    if not os.path.exists(token_path):
+        raise ConfigException("Service token file does not exist.")
+    if not os.path.exists(ca_path):
+        raise ConfigException("Service certification file does not exist.")
+    if ":" in host and not host.startswith("["):
+        host = f"[{host}]"
+    tok = _TokenFile(token_path, token_refresh_seconds)
+    try:
+        ctx = build_ssl_context(ca_file=ca_path)
+    except (ssl.SSLError, OSError) as exc:
+        raise ConfigException(f"in-cluster CA unusable: {exc}") from None
+    ns = None
+    ns_path = os.path.join(sa_dir, "namespace")
+    if os.path.exists(ns_path):
+        with open(ns_path, "r", encoding="utf-8") as fh:
+            ns = fh.read().strip()
+    return KubeEndpoint(server=f"https://{host}:{port}", ssl_context=ctx, header_provider=tok.headers,
+                        namespace=ns, source="in-cluster")

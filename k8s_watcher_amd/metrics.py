@@ -1,0 +1,158 @@
+"""Counters, latency histogram and Prometheus exposition.
+
+The reference has no metrics at all — only log lines. The watcher counts
+every stage of the pipeline and records the event→notify latency (socket read
+of the watch chunk → 2xx from clusterapi) in a log-bucketed histogram; when
+``record_samples`` is on (benchmarks) the raw samples are kept too so exact
+percentiles can be reported.
+
+Exposition uses the Prometheus text format directly (no client library
+needed); :func:`start_metrics_server` serves ``/metrics``, ``/healthz`` and
+``/readyz`` on a small asyncio HTTP server.
+"""
+
+from __future__ import annotations
+
+import array
+import asyncio
+import bisect
+import math
+import time
+from typing import Callable, Dict, List, Optional
+
+COUNTERS = (
+    "events_received",      # decoded watch events (incl. list-synthesised)
+    "events_filtered_critical",
+    "events_filtered_namespace",
+    "events_unchanged",     # dropped by notify_on=phase_change
+    "events_invalid",
+    "bookmarks",
+    "notify_submitted",
+    "notify_delivered",
+    "notify_failed",
+    "notify_retried",
+    "notify_superseded",
+    "notify_coalesced",
+    "watch_restarts",
+    "relists",
+    "expired_410",
+    "checkpoints_written",
+)
+
+# 1 µs .. ~100 s, 4 buckets per decade (upper bounds in ns)
+_BUCKETS_NS = [int(10 ** (3 + i / 4)) for i in range(0, 33)]
+
+
+class LatencyHistogram:
+    def __init__(self, record_samples: bool = False) -> None:
+        self.counts = [0] * (len(_BUCKETS_NS) + 1)
+        self.total_ns = 0
+        self.n = 0
+        self.samples: Optional[array.array] = array.array("q") if record_samples else None
+
+    def observe_ns(self, ns: int) -> None:
+        self.counts[bisect.bisect_left(_BUCKETS_NS, ns)] += 1
+        self.total_ns += ns
+        self.n += 1
+        if self.samples is not None:
+            self.samples.append(ns)
+
+    def reset(self) -> None:
+        self.counts = [0] * (len(_BUCKETS_NS) + 1)
+        self.total_ns = 0
+        self.n = 0
+        if self.samples is not None:
+            self.samples = array.array("q")
+
+    def percentile_ns(self, q: float) -> Optional[float]:
+        """Exact when samples are recorded, otherwise bucket upper bound."""
+        if self.n == 0:
+            return None
+        if self.samples is not None and len(self.samples):
+            s = sorted(self.samples)
+            k = max(0, min(len(s) - 1, int(math.ceil(q / 100.0 * len(s))) - 1))
+            return float(s[k])
+        target = q / 100.0 * self.n
+        acc = 0
+        for i, c in enumerate(self.counts):
+            acc += c
+            if acc >= target:
+                return float(_BUCKETS_NS[i] if i < len(_BUCKETS_NS) else _BUCKETS_NS[-1])
+        return float(_BUCKETS_NS[-1])
+
+
+class Metrics:
+    def __init__(self, record_samples: bool = False) -> None:
+        self.c: Dict[str, int] = {k: 0 for k in COUNTERS}
+        self.latency = LatencyHistogram(record_samples)
+        self.started = time.time()
+        self.ready = False
+        self.gauges: Dict[str, Callable[[], float]] = {}
+
+    def inc(self, name: str, n: int = 1) -> None:
+        self.c[name] = self.c.get(name, 0) + n
+
+    def snapshot(self) -> Dict[str, float]:
+        out: Dict[str, float] = dict(self.c)
+        for k, fn in self.gauges.items():
+            out[k] = fn()
+        p50 = self.latency.percentile_ns(50)
+        p99 = self.latency.percentile_ns(99)
+        out["notify_latency_p50_ms"] = p50 / 1e6 if p50 is not None else float("nan")
+        out["notify_latency_p99_ms"] = p99 / 1e6 if p99 is not None else float("nan")
+        return out
+
+    def prometheus_text(self) -> str:
+        lines: List[str] = []
+        for k, v in self.c.items():
+            name = f"k8s_watcher_{k}_total"
+            lines.append(f"# TYPE {name} counter")
+            lines.append(f"{name} {v}")
+        for k, fn in self.gauges.items():
+            name = f"k8s_watcher_{k}"
+            lines.append(f"# TYPE {name} gauge")
+            lines.append(f"{name} {fn()}")
+        h = self.latency
+        name = "k8s_watcher_notify_latency_seconds"
+        lines.append(f"# TYPE {name} histogram")
+        acc = 0
+        for ub, c in zip(_BUCKETS_NS, h.counts):
+            acc += c
+            lines.append(f'{name}_bucket{{le="{ub / 1e9:.9g}"}} {acc}')
+        lines.append(f'{name}_bucket{{le="+Inf"}} {h.n}')
+        lines.append(f"{name}_sum {h.total_ns / 1e9:.9f}")
+        lines.append(f"{name}_count {h.n}")
+        return "\n".join(lines) + "\n"
+
+
+async def start_metrics_server(metrics: Metrics, host: str, port: int) -> asyncio.AbstractServer:
+    """Tiny HTTP/1.1 server: ``/metrics``, ``/healthz``, ``/readyz`` (one request per connection)."""
+
+    async def handle(reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
+        try:
+            line = await asyncio.wait_for(reader.readline(), 10)
+            while True:
+                h = await asyncio.wait_for(reader.readline(), 10)
+                if h in (b"\r\n", b"\n", b""):
+                    break
+            parts = line.decode("latin-1").split()
+            path = parts[1] if len(parts) > 1 else "/"
+            if path.startswith("/metrics"):
+                status, body, ctype = "200 OK", metrics.prometheus_text(), "text/plain; version=0.0.4"
+            elif path.startswith("/healthz"):
+                status, body, ctype = "200 OK", "ok\n", "text/plain"
+            elif path.startswith("/readyz"):
+                status = "200 OK" if metrics.ready else "503 Service Unavailable"
+                body, ctype = ("ready\n" if metrics.ready else "not ready\n"), "text/plain"
+            else:
+                status, body, ctype = "404 Not Found", "not found\n", "text/plain"
+            data = body.encode()
+            writer.write(f"HTTP/1.1 {status}\r\nContent-Type: {ctype}\r\nContent-Length: {len(data)}\r\n"
+                         f"Connection: close\r\n\r\n".encode() + data)
+            await writer.drain()
+        except (asyncio.TimeoutError, ConnectionError):
+            pass
+        finally:
+            writer.close()
+
+    return await asyncio.start_server(handle, host, port)

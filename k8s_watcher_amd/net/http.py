@@ -1,0 +1,505 @@
+"""Minimal asyncio HTTP/1.1 client used for every network link.
+
+The reference delegates transport to ``kubernetes`` → urllib3 (watch stream)
+and ``requests`` (clusterapi POST), both blocking. Here one
+small ``asyncio.Protocol`` client serves both links so that
+
+* the watch stream hands *raw de-chunked bytes plus their socket-read
+  timestamp* straight to the event decoder (no line iterator, no model
+  classes), and
+* the notifier can keep many keep-alive connections busy from one thread.
+
+Supported: keep-alive pooling, ``Content-Length`` / ``chunked`` /
+read-until-close bodies, TLS through an ``ssl.SSLContext``, per-request
+timeouts and streaming responses.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import ssl as _ssl
+import time
+from typing import Callable, Dict, List, Optional, Tuple
+from urllib.parse import urlencode, urlsplit
+from ..utils.aio import with_timeout
+
+
+class HttpError(Exception):
+    """Transport-level failure (connect, reset, protocol violation, timeout)."""
+
+
+class HttpStatusError(HttpError):
+    """Non-success HTTP status where the caller asked for one to raise."""
+
+    def __init__(self, status: int, reason: str, body: bytes) -> None:
+        super().__init__(f"HTTP {status} {reason}: {body[:300]!r}")
+        self.status = status
+        self.reason = reason
+        self.body = body
+
+
+class Response:
+    __slots__ = ("status", "reason", "headers", "body")
+
+    def __init__(self, status: int, reason: str, headers: Dict[str, str], body: bytes) -> None:
+        self.status = status
+        self.reason = reason
+        self.headers = headers
+        self.body = body
+
+    @property
+    def ok(self) -> bool:
+        return 200 <= self.status < 300
+
+    def text(self) -> str:
+        return self.body.decode("utf-8", "replace")
+
+    def json(self):
+        import json
+        return json.loads(self.body)
+
+
+class ResponseParser:
+    """Incremental HTTP/1.1 response parser.
+
+    ``feed(data)`` consumes bytes; body bytes go to ``on_body`` (if set) or are
+    accumulated. ``on_head`` fires once the status line + headers are parsed;
+    ``on_complete`` when the message is done. ``no_body`` must be set for
+    responses to HEAD requests.
+    """
+
+    HEAD, LENGTH, CHUNK_SIZE, CHUNK_DATA, CHUNK_CRLF, TRAILER, UNTIL_CLOSE, DONE = range(8)
+
+    def __init__(self) -> None:
+        self.reset()
+
+    def reset(self, no_body: bool = False) -> None:
+        self.state = self.HEAD
+        self.buf = bytearray()
+        self.status = 0
+        self.reason = ""
+        self.headers: Dict[str, str] = {}
+        self.remaining = 0
+        self.body_parts: List[bytes] = []
+        self.keep_alive = True
+        self.no_body = no_body
+        self.on_head: Optional[Callable[["ResponseParser"], None]] = None
+        self.on_body: Optional[Callable[[bytes], None]] = None
+        self.on_complete: Optional[Callable[["ResponseParser"], None]] = None
+
+    # ------------------------------------------------------------------ helpers
+    def _emit(self, data: bytes) -> None:
+        if not data:
+            return
+        if self.on_body is not None:
+            self.on_body(data)
+        else:
+            self.body_parts.append(data)
+
+    def body(self) -> bytes:
+        return b"".join(self.body_parts)
+
+    def _finish(self) -> None:
+        self.state = self.DONE
+        if self.on_complete is not None:
+            self.on_complete(self)
+
+    def _parse_head(self, head: bytes) -> None:
+        lines = head.split(b"\r\n")
+        status_line = lines[0].decode("latin-1")
+        parts = status_line.split(" ", 2)
+        if len(parts) < 2 or not parts[0].startswith("HTTP/"):
+            raise HttpError(f"malformed status line {status_line!r}")
+        version = parts[0]
+        self.status = int(parts[1])
+        self.reason = parts[2] if len(parts) > 2 else ""
+        hdrs: Dict[str, str] = {}
+        for raw in lines[1:]:
+            if not raw:
+                continue
+            k, _, v = raw.decode("latin-1").partition(":")
+            k = k.strip().lower()
+            v = v.strip()
+            if k in hdrs:
+                hdrs[k] = hdrs[k] + ", " + v
+            else:
+                hdrs[k] = v
+        self.headers = hdrs
+        conn = hdrs.get("connection", "").lower()
+        if version == "HTTP/1.0":
+            self.keep_alive = "keep-alive" in conn
+        else:
+            self.keep_alive = "close" not in conn
+        if self.no_body or self.status in (204, 304) or 100 <= self.status < 200:
+            self.state = self.DONE
+        elif "chunked" in hdrs.get("transfer-encoding", "").lower():
+            self.state = self.CHUNK_SIZE
+        elif "content-length" in hdrs:
+            self.remaining = int(hdrs["content-length"])
+            self.state = self.LENGTH if self.remaining > 0 else self.DONE
+        else:
+            self.state = self.UNTIL_CLOSE
+            self.keep_alive = False
+
+    # ------------------------------------------------------------------ feeding
+    def feed(self, data: bytes) -> bytes:
+        """Consume ``data``; returns bytes left over after a complete message."""
+        buf = self.buf
+        buf += data
+        pos = 0
+        n = len(buf)
+        while True:
+            st = self.state
+            if st == self.HEAD:
+                idx = buf.find(b"\r\n\r\n", pos)
+                if idx < 0:
+                    break
+                self._parse_head(bytes(buf[pos:idx]))
+                pos = idx + 4
+                if self.on_head is not None:
+                    self.on_head(self)
+                if self.state == self.DONE:
+                    self._finish()
+                    break
+            elif st == self.LENGTH:
+                take = min(self.remaining, n - pos)
+                if take <= 0:
+                    break
+                self._emit(bytes(buf[pos:pos + take]))
+                pos += take
+                self.remaining -= take
+                if self.remaining == 0:
+                    self._finish()
+                    break
+            elif st == self.CHUNK_SIZE:
+                idx = buf.find(b"\r\n", pos)
+                if idx < 0:
+                    break
+                line = bytes(buf[pos:idx]).split(b";", 1)[0].strip()
+                try:
+                    size = int(line, 16)
+                except ValueError:
+                    raise HttpError(f"bad chunk size line {line!r}") from None
+                pos = idx + 2
+                if size == 0:
+                    self.state = self.TRAILER
+                else:
+                    self.remaining = size
+                    self.state = self.CHUNK_DATA
+            elif st == self.CHUNK_DATA:
+                take = min(self.remaining, n - pos)
+                if take <= 0:
+                    break
+                self._emit(bytes(buf[pos:pos + take]))
+                pos += take
+                self.remaining -= take
+                if self.remaining == 0:
+                    self.state = self.CHUNK_CRLF
+            elif st == self.CHUNK_CRLF:
+                if n - pos < 2:
+                    break
+                pos += 2
+                self.state = self.CHUNK_SIZE
+            elif st == self.TRAILER:
+                idx = buf.find(b"\r\n", pos)
+                if idx < 0:
+                    break
+                empty = idx == pos
+                pos = idx + 2
+                if empty:
+                    self._finish()
+                    break
+            elif st == self.UNTIL_CLOSE:
+                if pos < n:
+                    self._emit(bytes(buf[pos:]))
+                    pos = n
+                break
+            else:  # DONE
+                break
+        rest = b""
+        if self.state == self.DONE:
+            rest = bytes(buf[pos:])
+            self.buf = bytearray()
+        else:
+            del buf[:pos]
+        return rest
+
+    def feed_eof(self) -> None:
+        if self.state == self.UNTIL_CLOSE:
+            self._finish()
+        elif self.state != self.DONE:
+            raise HttpError("connection closed mid-response")
+
+
+class _ClientProtocol(asyncio.Protocol):
+    """One TCP/TLS connection; at most one outstanding request (no pipelining here)."""
+
+    def __init__(self, loop: asyncio.AbstractEventLoop) -> None:
+        self.loop = loop
+        self.transport: Optional[asyncio.Transport] = None
+        self.parser = ResponseParser()
+        self.waiter: Optional[asyncio.Future] = None
+        self.closed = loop.create_future()
+        self.busy = False
+        self.stream_sink: Optional[Callable[[bytes, int], None]] = None
+        self.stream_head: Optional[asyncio.Future] = None
+        self.last_activity = time.monotonic()
+
+    # asyncio callbacks
+    def connection_made(self, transport) -> None:  # type: ignore[override]
+        self.transport = transport
+
+    def data_received(self, data: bytes) -> None:  # type: ignore[override]
+        self.last_activity = time.monotonic()
+        try:
+            if self.stream_sink is not None:
+                stamp = time.monotonic_ns()
+                sink = self.stream_sink
+                self.parser.on_body = lambda b: sink(b, stamp)
+            self.parser.feed(data)
+        except Exception as exc:  # noqa: BLE001
+            self._fail(exc)
+            if self.transport is not None:
+                self.transport.close()
+
+    def connection_lost(self, exc) -> None:  # type: ignore[override]
+        try:
+            self.parser.feed_eof()
+        except Exception as err:  # noqa: BLE001
+            self._fail(err if exc is None else HttpError(str(exc)))
+        if not self.closed.done():
+            self.closed.set_result(None)
+        self._fail(HttpError("connection closed"))
+
+    def _fail(self, exc: BaseException) -> None:
+        for fut in (self.stream_head, self.waiter):
+            if fut is not None and not fut.done():
+                fut.set_exception(exc if isinstance(exc, HttpError) else HttpError(repr(exc)))
+
+    # request helpers
+    def is_reusable(self) -> bool:
+        return (self.transport is not None and not self.transport.is_closing()
+                and not self.busy and self.parser.keep_alive)
+
+    def close(self) -> None:
+        if self.transport is not None:
+            self.transport.close()
+
+
+def build_request(method: str, target: str, host_header: str, headers: Dict[str, str],
+                  body: Optional[bytes]) -> bytes:
+    lines = [f"{method} {target} HTTP/1.1", f"Host: {host_header}"]
+    for k, v in headers.items():
+        lines.append(f"{k}: {v}")
+    if body is not None:
+        lines.append(f"Content-Length: {len(body)}")
+    head = ("\r\n".join(lines) + "\r\n\r\n").encode("latin-1")
+    return head + body if body else head
+
+
+class StreamResponse:
+    """A response whose body is delivered incrementally to a sink callback."""
+
+    def __init__(self, proto: _ClientProtocol, status: int, reason: str, headers: Dict[str, str]) -> None:
+        self._proto = proto
+        self.status = status
+        self.reason = reason
+        self.headers = headers
+
+    @property
+    def finished(self) -> "asyncio.Future":
+        """Resolves when the server ends the body or the connection closes."""
+        return self._proto.closed
+
+    @property
+    def last_activity(self) -> float:
+        return self._proto.last_activity
+
+    def close(self) -> None:
+        self._proto.stream_sink = None
+        self._proto.close()
+
+
+class HttpClient:
+    """Pooled keep-alive HTTP/1.1 client for one origin (scheme://host:port)."""
+
+    def __init__(self, base_url: str, ssl_context: Optional[_ssl.SSLContext] = None,
+                 headers: Optional[Dict[str, str]] = None, timeout: float = 30.0,
+                 header_provider: Optional[Callable[[], Dict[str, str]]] = None,
+                 max_idle: int = 8) -> None:
+        u = urlsplit(base_url)
+        if u.scheme not in ("http", "https"):
+            raise ValueError(f"unsupported URL scheme in {base_url!r}")
+        self.scheme = u.scheme
+        self.host = u.hostname or "localhost"
+        self.port = u.port or (443 if u.scheme == "https" else 80)
+        self.base_path = u.path.rstrip("/")
+        default_port = 443 if u.scheme == "https" else 80
+        self.host_header = self.host if self.port == default_port else f"{self.host}:{self.port}"
+        if ":" in self.host and not self.host.startswith("["):  # IPv6 literal
+            self.host_header = f"[{self.host}]" + ("" if self.port == default_port else f":{self.port}")
+        if u.scheme == "https" and ssl_context is None:
+            ssl_context = _ssl.create_default_context()
+        self.ssl_context = ssl_context if u.scheme == "https" else None
+        self.headers = dict(headers or {})
+        self.header_provider = header_provider
+        self.timeout = timeout
+        self.max_idle = max_idle
+        self._idle: List[_ClientProtocol] = []
+        self._all: List[_ClientProtocol] = []
+
+    # ------------------------------------------------------------------ plumbing
+    def url_target(self, path: str, query: Optional[Dict[str, object]] = None) -> str:
+        target = self.base_path + path
+        if query:
+            q = {k: ("true" if v is True else "false" if v is False else v)
+                 for k, v in query.items() if v is not None}
+            if q:
+                target += "?" + urlencode(q)
+        return target
+
+    def _merged_headers(self, extra: Optional[Dict[str, str]]) -> Dict[str, str]:
+        h = dict(self.headers)
+        if self.header_provider is not None:
+            h.update(self.header_provider())
+        if extra:
+            h.update(extra)
+        return h
+
+    async def _connect(self, timeout: float) -> _ClientProtocol:
+        loop = asyncio.get_running_loop()
+        try:
+            _, proto = await with_timeout(
+                loop.create_connection(lambda: _ClientProtocol(loop), self.host, self.port,
+                                       ssl=self.ssl_context,
+                                       server_hostname=self.host if self.ssl_context else None),
+                timeout)
+        except asyncio.TimeoutError:
+            raise HttpError(f"connect to {self.host}:{self.port} timed out") from None
+        except OSError as exc:
+            raise HttpError(f"connect to {self.host}:{self.port} failed: {exc}") from None
+        self._all.append(proto)
+        return proto
+
+    async def _acquire(self, timeout: float) -> _ClientProtocol:
+        while self._idle:
+            proto = self._idle.pop()
+            if proto.is_reusable():
+                return proto
+        return await self._connect(timeout)
+
+    def _release(self, proto: _ClientProtocol) -> None:
+        proto.busy = False
+        if proto.is_reusable() and len(self._idle) < self.max_idle:
+            self._idle.append(proto)
+        else:
+            proto.close()
+            self._forget(proto)
+
+    def _forget(self, proto: _ClientProtocol) -> None:
+        try:
+            self._all.remove(proto)
+        except ValueError:
+            pass
+
+    # ------------------------------------------------------------------ API
+    async def request(self, method: str, path: str, query: Optional[Dict[str, object]] = None,
+                      headers: Optional[Dict[str, str]] = None, body: Optional[bytes] = None,
+                      timeout: Optional[float] = None) -> Response:
+        tmo = self.timeout if timeout is None else timeout
+        target = self.url_target(path, query)
+        raw = build_request(method, target, self.host_header, self._merged_headers(headers), body)
+        for attempt in (0, 1):
+            proto = await self._acquire(tmo)
+            reused = attempt == 0 and proto in self._all and proto.parser.state == ResponseParser.DONE
+            loop = asyncio.get_running_loop()
+            proto.busy = True
+            proto.parser.reset(no_body=(method == "HEAD"))
+            fut = loop.create_future()
+            proto.waiter = fut
+            proto.stream_sink = None
+
+            def _done(p: ResponseParser, f=fut) -> None:
+                if not f.done():
+                    f.set_result(Response(p.status, p.reason, p.headers, p.body()))
+
+            proto.parser.on_complete = _done
+            assert proto.transport is not None
+            proto.transport.write(raw)
+            try:
+                resp = await with_timeout(fut, tmo)
+            except asyncio.TimeoutError:
+                proto.close()
+                self._forget(proto)
+                raise HttpError(f"{method} {target} timed out after {tmo}s") from None
+            except HttpError:
+                proto.close()
+                self._forget(proto)
+                if reused and method in ("GET", "HEAD"):
+                    continue  # stale keep-alive socket: retry once on a fresh one
+                raise
+            self._release(proto)
+            return resp
+        raise HttpError("unreachable")
+
+    async def stream(self, method: str, path: str, sink: Callable[[bytes, int], None],
+                     query: Optional[Dict[str, object]] = None,
+                     headers: Optional[Dict[str, str]] = None,
+                     timeout: Optional[float] = None) -> Tuple[StreamResponse, Optional[bytes]]:
+        """Start a request whose body is streamed to ``sink(data, read_ns)``.
+
+        Returns ``(stream, error_body)``: for a non-2xx status the whole body
+        is read and returned as ``error_body`` and the connection is closed.
+        """
+        tmo = self.timeout if timeout is None else timeout
+        target = self.url_target(path, query)
+        raw = build_request(method, target, self.host_header, self._merged_headers(headers), None)
+        proto = await self._connect(tmo)
+        loop = asyncio.get_running_loop()
+        proto.busy = True
+        head_fut = loop.create_future()
+        proto.stream_head = head_fut
+        parser = proto.parser
+        parser.reset()
+        err_parts: List[bytes] = []
+
+        def _on_head(p: ResponseParser) -> None:
+            if not (200 <= p.status < 300):
+                proto.stream_sink = None
+                p.on_body = err_parts.append
+                p.on_complete = lambda _p: (not head_fut.done()) and head_fut.set_result(False)
+                return
+            if not head_fut.done():
+                head_fut.set_result(True)
+
+        def _on_complete(_p: ResponseParser) -> None:
+            proto.close()
+
+        parser.on_head = _on_head
+        parser.on_complete = _on_complete
+        proto.stream_sink = sink
+        assert proto.transport is not None
+        proto.transport.write(raw)
+        try:
+            good = await with_timeout(head_fut, tmo)
+        except asyncio.TimeoutError:
+            proto.close()
+            self._forget(proto)
+            raise HttpError(f"{method} {target}: no response head within {tmo}s") from None
+        except HttpError:
+            proto.close()
+            self._forget(proto)
+            raise
+        sr = StreamResponse(proto, parser.status, parser.reason, parser.headers)
+        if not good:
+            proto.close()
+            self._forget(proto)
+            return sr, b"".join(err_parts)
+        return sr, None
+
+    async def close(self) -> None:
+        for proto in list(self._all):
+            proto.close()
+        self._all.clear()
+        self._idle.clear()
+        await asyncio.sleep(0)

@@ -1,0 +1,1185 @@
+// _kwcore — native watch-event decoder for k8s-watcher-amd.
+//
+// Hot path of the watcher: one kube-apiserver watch line
+// `{"type":"MODIFIED","object":{<Pod>}}` → the fields the filters need plus the
+// clusterapi payload *core* (reference
+// /root/reference/watcher/pod_watcher.py:159-202) as ready-to-send JSON bytes.
+//
+// The reference pays for this with json.loads + reflective V1Pod model
+// construction inside the `kubernetes` library and then a Python dict build;
+// here a single forward pass over the line records byte spans of the ~20
+// fields that matter, skips everything else (managedFields, volumes, env, ...)
+// with a structural scanner, and assembles the payload by copying raw JSON
+// tokens. No Python object is created for the pod body.
+//
+// Semantics are pinned to the Python engine (models/payload.py::build_core),
+// see tests/test_native_parity.py.
+
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
+
+namespace {
+
+// ----------------------------------------------------------------------------- spans
+
+struct Span {
+    const char* p = nullptr;  // raw JSON token (strings include their quotes)
+    size_t n = 0;
+    bool present() const { return p != nullptr; }
+    bool is_null() const { return p && n == 4 && std::memcmp(p, "null", 4) == 0; }
+    bool is_string() const { return p && n >= 2 && p[0] == '"'; }
+};
+
+struct Condition { Span type, status, reason, message; };
+struct CStatus { Span name, ready, restart_count, state; };
+struct Container { Span name, image; };
+
+struct PodSpans {
+    bool meta_present = false;
+    Span name, ns, uid, rv, labels, annotations, ctime;
+    bool spec_present = false;
+    Span node_name;
+    std::vector<Container> containers;
+    bool status_present = false;
+    Span phase;
+    std::vector<Condition> conditions;
+    std::vector<CStatus> cstatuses;
+    void clear() {
+        meta_present = spec_present = status_present = false;
+        name = ns = uid = rv = labels = annotations = ctime = node_name = phase = Span();
+        containers.clear();
+        conditions.clear();
+        cstatuses.clear();
+    }
+};
+
+struct ParseError {
+    const char* msg;
+};
+
+// ----------------------------------------------------------------------------- scanner
+
+class Parser {
+  public:
+    Parser(const char* b, const char* e) : p_(b), end_(e) {}
+    const char* p_;
+    const char* end_;
+
+    [[noreturn]] void fail(const char* m) { throw ParseError{m}; }
+
+    inline void ws() {
+        while (p_ < end_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_;
+    }
+    inline char peek() {
+        ws();
+        if (p_ >= end_) fail("unexpected end of input");
+        return *p_;
+    }
+    inline void expect(char c) {
+        if (peek() != c) fail("unexpected character");
+        ++p_;
+    }
+
+    // Returns pointer one past the closing quote of the string starting at p_ ('"').
+    inline const char* string_end(const char* s) {
+        ++s;  // opening quote
+#if defined(__x86_64__)
+        if (use_avx2) return string_end_avx2(s);
+#endif
+        while (s < end_) {
+            char c = *s;
+            if (c == '"') return s + 1;
+            if (c == '\\') {
+                s += 2;
+                continue;
+            }
+            ++s;
+        }
+        fail("unterminated string");
+    }
+
+#if defined(__x86_64__)
+    static bool use_avx2;
+    __attribute__((target("avx2,bmi,bmi2"))) const char* string_end_avx2(const char* s) {
+        const __m256i q = _mm256_set1_epi8('"');
+        const __m256i bs = _mm256_set1_epi8('\\');
+        while (s + 32 <= end_) {
+            __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s));
+            uint32_t mq = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, q));
+            uint32_t mb = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, bs));
+            if (mb == 0) {
+                if (mq) return s + __builtin_ctz(mq) + 1;
+                s += 32;
+                continue;
+            }
+            uint32_t first_b = __builtin_ctz(mb);
+            if (mq && (uint32_t)__builtin_ctz(mq) < first_b) return s + __builtin_ctz(mq) + 1;
+            s += first_b + 2;  // skip the escape pair, rescan from there
+        }
+        while (s < end_) {
+            char c = *s;
+            if (c == '"') return s + 1;
+            if (c == '\\') {
+                s += 2;
+                continue;
+            }
+            ++s;
+        }
+        fail("unterminated string");
+    }
+
+    // Skip a balanced {...} or [...] starting at s (which points at the opener).
+    __attribute__((target("avx2,bmi,bmi2"))) const char* skip_container_avx2(const char* s) {
+        int depth = 0;
+        const __m256i q = _mm256_set1_epi8('"');
+        const __m256i ob = _mm256_set1_epi8('{');
+        const __m256i cb = _mm256_set1_epi8('}');
+        const __m256i os = _mm256_set1_epi8('[');
+        const __m256i cs = _mm256_set1_epi8(']');
+        while (s + 32 <= end_) {
+            __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s));
+            uint32_t m = (uint32_t)_mm256_movemask_epi8(
+                _mm256_or_si256(_mm256_or_si256(_mm256_cmpeq_epi8(v, q), _mm256_cmpeq_epi8(v, ob)),
+                                _mm256_or_si256(_mm256_cmpeq_epi8(v, cb),
+                                                _mm256_or_si256(_mm256_cmpeq_epi8(v, os),
+                                                                _mm256_cmpeq_epi8(v, cs)))));
+            const char* next = s + 32;
+            while (m) {
+                uint32_t i = __builtin_ctz(m);
+                const char* c = s + i;
+                char ch = *c;
+                if (ch == '"') {
+                    const char* after = string_end_avx2(c + 1);
+                    if (after > s + 32) {
+                        next = after;
+                        m = 0;
+                        break;
+                    }
+                    // clear bits up to and including the closing quote
+                    uint32_t upto = (uint32_t)(after - s);
+                    m = upto >= 32 ? 0 : (m & ~((1u << upto) - 1u));
+                    if (upto >= 32) {
+                        next = after;
+                        break;
+                    }
+                    continue;
+                }
+                if (ch == '{' || ch == '[') {
+                    ++depth;
+                } else {
+                    if (--depth == 0) return c + 1;
+                }
+                m &= m - 1;
+            }
+            s = next;
+        }
+        return skip_container_scalar(s, depth);
+    }
+#endif
+
+    const char* skip_container_scalar(const char* s, int depth) {
+        while (s < end_) {
+            char c = *s;
+            if (c == '"') {
+                s = string_end_scalar(s + 1);
+                continue;
+            }
+            if (c == '{' || c == '[') {
+                ++depth;
+            } else if (c == '}' || c == ']') {
+                if (--depth == 0) return s + 1;
+            }
+            ++s;
+        }
+        fail("unterminated container");
+    }
+
+    const char* string_end_scalar(const char* s) {
+        while (s < end_) {
+            char c = *s;
+            if (c == '"') return s + 1;
+            if (c == '\\') {
+                s += 2;
+                continue;
+            }
+            ++s;
+        }
+        fail("unterminated string");
+    }
+
+    // Skip any JSON value at p_ and return its raw span.
+    Span value() {
+        char c = peek();
+        Span sp;
+        sp.p = p_;
+        if (c == '"') {
+            p_ = string_end(p_);
+        } else if (c == '{' || c == '[') {
+#if defined(__x86_64__)
+            p_ = use_avx2 ? skip_container_avx2(p_) : skip_container_scalar(p_, 0);
+#else
+            p_ = skip_container_scalar(p_, 0);
+#endif
+        } else {
+            while (p_ < end_) {
+                char d = *p_;
+                if (d == ',' || d == '}' || d == ']' || d == ' ' || d == '\n' || d == '\r' || d == '\t') break;
+                ++p_;
+            }
+            if (p_ == sp.p) fail("empty value");
+        }
+        sp.n = (size_t)(p_ - sp.p);
+        return sp;
+    }
+
+    // Read an object key (raw, without quotes; escapes left as-is — keys we
+    // match never contain escapes) and consume the following ':'.
+    inline void key(const char*& k, size_t& kn) {
+        if (peek() != '"') fail("expected key");
+        const char* s = p_ + 1;
+        p_ = string_end(p_);
+        k = s;
+        kn = (size_t)(p_ - 1 - s);
+        expect(':');
+    }
+
+    // Iterate an object: f(key, keylen) must consume the value.
+    template <class F>
+    void object(F&& f) {
+        expect('{');
+        if (peek() == '}') {
+            ++p_;
+            return;
+        }
+        while (true) {
+            const char* k;
+            size_t kn;
+            key(k, kn);
+            f(k, kn);
+            char c = peek();
+            ++p_;
+            if (c == '}') return;
+            if (c != ',') fail("expected , or }");
+        }
+    }
+
+    template <class F>
+    void array(F&& f) {
+        expect('[');
+        if (peek() == ']') {
+            ++p_;
+            return;
+        }
+        while (true) {
+            f();
+            char c = peek();
+            ++p_;
+            if (c == ']') return;
+            if (c != ',') fail("expected , or ]");
+        }
+    }
+
+    bool null_here() {
+        if (peek() == 'n' && end_ - p_ >= 4 && std::memcmp(p_, "null", 4) == 0) {
+            p_ += 4;
+            return true;
+        }
+        return false;
+    }
+};
+
+#if defined(__x86_64__)
+bool Parser::use_avx2 = false;
+#endif
+
+#define KEYIS(lit) (kn == sizeof(lit) - 1 && std::memcmp(k, lit, sizeof(lit) - 1) == 0)
+
+void parse_metadata(Parser& P, PodSpans& S) {
+    if (P.null_here()) return;
+    S.meta_present = true;
+    P.object([&](const char* k, size_t kn) {
+        switch (kn) {
+            case 3:
+                if (KEYIS("uid")) { S.uid = P.value(); return; }
+                break;
+            case 4:
+                if (KEYIS("name")) { S.name = P.value(); return; }
+                break;
+            case 6:
+                if (KEYIS("labels")) { S.labels = P.value(); return; }
+                break;
+            case 9:
+                if (KEYIS("namespace")) { S.ns = P.value(); return; }
+                break;
+            case 11:
+                if (KEYIS("annotations")) { S.annotations = P.value(); return; }
+                break;
+            case 15:
+                if (KEYIS("resourceVersion")) { S.rv = P.value(); return; }
+                break;
+            case 17:
+                if (KEYIS("creationTimestamp")) { S.ctime = P.value(); return; }
+                break;
+        }
+        P.value();
+    });
+}
+
+void parse_spec(Parser& P, PodSpans& S) {
+    if (P.null_here()) return;
+    S.spec_present = true;
+    P.object([&](const char* k, size_t kn) {
+        if (KEYIS("nodeName")) {
+            S.node_name = P.value();
+        } else if (KEYIS("containers")) {
+            if (P.null_here()) return;
+            if (P.peek() != '[') { P.value(); return; }
+            S.containers.clear();  // duplicate key: last wins
+            P.array([&]() {
+                if (P.peek() != '{') { P.value(); return; }
+                Container c;
+                P.object([&](const char* k2, size_t kn2) {
+                    const char* k = k2; size_t kn = kn2;
+                    if (KEYIS("name")) c.name = P.value();
+                    else if (KEYIS("image")) c.image = P.value();
+                    else P.value();
+                });
+                S.containers.push_back(c);
+            });
+        } else {
+            P.value();
+        }
+    });
+}
+
+void parse_status(Parser& P, PodSpans& S) {
+    if (P.null_here()) return;
+    S.status_present = true;
+    P.object([&](const char* k, size_t kn) {
+        if (KEYIS("phase")) {
+            S.phase = P.value();
+        } else if (KEYIS("conditions")) {
+            if (P.null_here()) return;
+            if (P.peek() != '[') { P.value(); return; }
+            S.conditions.clear();
+            P.array([&]() {
+                if (P.peek() != '{') { P.value(); return; }
+                Condition c;
+                P.object([&](const char* k2, size_t kn2) {
+                    const char* k = k2; size_t kn = kn2;
+                    if (KEYIS("type")) c.type = P.value();
+                    else if (KEYIS("status")) c.status = P.value();
+                    else if (KEYIS("reason")) c.reason = P.value();
+                    else if (KEYIS("message")) c.message = P.value();
+                    else P.value();
+                });
+                S.conditions.push_back(c);
+            });
+        } else if (KEYIS("containerStatuses")) {
+            if (P.null_here()) return;
+            if (P.peek() != '[') { P.value(); return; }
+            S.cstatuses.clear();
+            P.array([&]() {
+                if (P.peek() != '{') { P.value(); return; }
+                CStatus c;
+                P.object([&](const char* k2, size_t kn2) {
+                    const char* k = k2; size_t kn = kn2;
+                    if (KEYIS("name")) c.name = P.value();
+                    else if (KEYIS("ready")) c.ready = P.value();
+                    else if (KEYIS("restartCount")) c.restart_count = P.value();
+                    else if (KEYIS("state")) c.state = P.value();
+                    else P.value();
+                });
+                S.cstatuses.push_back(c);
+            });
+        } else {
+            P.value();
+        }
+    });
+}
+
+void parse_pod(Parser& P, PodSpans& S) {
+    P.object([&](const char* k, size_t kn) {
+        if (KEYIS("metadata")) {
+            if (P.peek() == '{' || P.peek() == 'n') parse_metadata(P, S); else P.value();
+        } else if (KEYIS("spec")) {
+            if (P.peek() == '{' || P.peek() == 'n') parse_spec(P, S); else P.value();
+        } else if (KEYIS("status")) {
+            if (P.peek() == '{' || P.peek() == 'n') parse_status(P, S); else P.value();
+        } else {
+            P.value();
+        }
+    });
+}
+
+// ----------------------------------------------------------------------------- output
+
+inline void put(std::string& o, const char* s, size_t n) { o.append(s, n); }
+inline void put(std::string& o, const char* lit) { o.append(lit); }
+inline void raw_or_null(std::string& o, const Span& s) {
+    if (s.present()) o.append(s.p, s.n); else o.append("null", 4);
+}
+
+// JSON "falsy" per Python truthiness after json.loads: null, {}, [], "", 0, false.
+bool falsy_token(const Span& s) {
+    if (!s.present()) return true;
+    const char* p = s.p;
+    size_t n = s.n;
+    if (n == 4 && std::memcmp(p, "null", 4) == 0) return true;
+    if (n == 5 && std::memcmp(p, "false", 5) == 0) return true;
+    if (n == 2 && std::memcmp(p, "\"\"", 2) == 0) return true;
+    if (p[0] == '{' || p[0] == '[') {
+        for (size_t i = 1; i + 1 < n; ++i) {
+            char c = p[i];
+            if (!(c == ' ' || c == '\n' || c == '\r' || c == '\t')) return false;
+        }
+        return true;
+    }
+    if (p[0] == '0' || p[0] == '-') {
+        for (size_t i = 0; i < n; ++i) {
+            char c = p[i];
+            if (c != '0' && c != '-' && c != '.' && c != 'e' && c != 'E' && c != '+') return false;
+        }
+        return true;
+    }
+    return false;
+}
+
+bool is_digit(char c) { return c >= '0' && c <= '9'; }
+
+// models/timefmt.py::k8s_time_to_isoformat on the raw string token.
+void creation_time(std::string& o, const Span& s) {
+    if (!s.present() || s.is_null()) {
+        o.append("null", 4);
+        return;
+    }
+    if (!s.is_string()) {  // non-string: passed through unchanged
+        o.append(s.p, s.n);
+        return;
+    }
+    const char* p = s.p + 1;
+    size_t n = s.n - 2;
+    for (size_t i = 0; i < n; ++i)
+        if (p[i] == '\\') {  // never produced by the API; keep verbatim
+            o.append(s.p, s.n);
+            return;
+        }
+    // YYYY-MM-DD[Tt ]HH:MM:SS(.frac)?(Z|z|[+-]HH:?MM)?
+    auto digits = [&](size_t at, size_t cnt) {
+        if (at + cnt > n) return false;
+        for (size_t i = 0; i < cnt; ++i)
+            if (!is_digit(p[at + i])) return false;
+        return true;
+    };
+    bool ok = n >= 19 && digits(0, 4) && p[4] == '-' && digits(5, 2) && p[7] == '-' && digits(8, 2) &&
+              (p[10] == 'T' || p[10] == 't' || p[10] == ' ') && digits(11, 2) && p[13] == ':' &&
+              digits(14, 2) && p[16] == ':' && digits(17, 2);
+    size_t i = 19;
+    size_t fs = 0, fn = 0;
+    if (ok && i < n && p[i] == '.') {
+        fs = ++i;
+        while (i < n && is_digit(p[i])) ++i;
+        fn = i - fs;
+        if (fn == 0) ok = false;
+    }
+    std::string tz;
+    bool has_tz = false;
+    if (ok && i < n) {
+        if ((p[i] == 'Z' || p[i] == 'z') && i + 1 == n) {
+            tz = "+00:00";
+            has_tz = true;
+        } else if ((p[i] == '+' || p[i] == '-') && (n - i == 6 || n - i == 5)) {
+            if (n - i == 6 && digits(i + 1, 2) && p[i + 3] == ':' && digits(i + 4, 2)) {
+                tz.assign(p + i, 6);
+            } else if (n - i == 5 && digits(i + 1, 4)) {
+                tz.assign(p + i, 3);
+                tz.push_back(':');
+                tz.append(p + i + 3, 2);
+            } else {
+                ok = false;
+            }
+            if (tz == "-00:00") tz = "+00:00";
+            has_tz = true;
+        } else {
+            ok = false;
+        }
+    }
+    if (!ok) {
+        o.append(s.p, s.n);
+        return;
+    }
+    o.push_back('"');
+    o.append(p, 10);
+    o.push_back('T');
+    o.append(p + 11, 8);
+    if (fn) {
+        char micro[7];
+        for (size_t k = 0; k < 6; ++k) micro[k] = k < fn ? p[fs + k] : '0';
+        micro[6] = 0;
+        bool nonzero = false;
+        for (size_t k = 0; k < 6; ++k)
+            if (micro[k] != '0') nonzero = true;
+        if (nonzero) {
+            o.push_back('.');
+            o.append(micro, 6);
+        }
+    }
+    if (has_tz) o.append(tz);
+    o.push_back('"');
+}
+
+void build_core(std::string& o, const PodSpans& S, const std::string& env_json) {
+    o.clear();
+    o.append("{\"name\":");
+    raw_or_null(o, S.name);
+    o.append(",\"namespace\":");
+    raw_or_null(o, S.ns);
+    o.append(",\"uid\":");
+    raw_or_null(o, S.uid);
+    o.append(",\"environment\":");
+    o.append(env_json);
+    o.append(",\"status\":{\"phase\":");
+    if (S.status_present) {
+        raw_or_null(o, S.phase);
+        o.append(",\"conditions\":[");
+        bool first = true;
+        for (const auto& c : S.conditions) {
+            if (!first) o.push_back(',');
+            first = false;
+            o.append("{\"type\":");
+            raw_or_null(o, c.type);
+            o.append(",\"status\":");
+            raw_or_null(o, c.status);
+            o.append(",\"reason\":");
+            raw_or_null(o, c.reason);
+            o.append(",\"message\":");
+            raw_or_null(o, c.message);
+            o.push_back('}');
+        }
+        o.append("],\"container_statuses\":[");
+        first = true;
+        for (const auto& c : S.cstatuses) {
+            if (!first) o.push_back(',');
+            first = false;
+            o.append("{\"name\":");
+            raw_or_null(o, c.name);
+            o.append(",\"ready\":");
+            raw_or_null(o, c.ready);
+            o.append(",\"restart_count\":");
+            raw_or_null(o, c.restart_count);
+            o.append(",\"state\":");
+            raw_or_null(o, c.state);
+            o.push_back('}');
+        }
+        o.append("]}");
+    } else {
+        o.append("\"Unknown\",\"conditions\":[],\"container_statuses\":[]}");
+    }
+    o.append(",\"spec\":{\"node_name\":");
+    if (S.spec_present) {
+        raw_or_null(o, S.node_name);
+        o.append(",\"containers\":[");
+        bool first = true;
+        for (const auto& c : S.containers) {
+            if (!first) o.push_back(',');
+            first = false;
+            o.append("{\"name\":");
+            raw_or_null(o, c.name);
+            o.append(",\"image\":");
+            raw_or_null(o, c.image);
+            o.push_back('}');
+        }
+        o.append("]}");
+    } else {
+        o.append("null,\"containers\":[]}");
+    }
+    o.append(",\"metadata\":{\"labels\":");
+    if (falsy_token(S.labels)) o.append("{}"); else o.append(S.labels.p, S.labels.n);
+    o.append(",\"annotations\":");
+    if (falsy_token(S.annotations)) o.append("{}"); else o.append(S.annotations.p, S.annotations.n);
+    o.append(",\"creation_timestamp\":");
+    creation_time(o, S.ctime);
+    o.append("}}");
+}
+
+// ----------------------------------------------------------------------------- Python glue
+
+PyObject* g_json_loads = nullptr;
+PyObject* g_types[6];  // ADDED MODIFIED DELETED BOOKMARK ERROR INVALID
+enum { T_ADDED, T_MODIFIED, T_DELETED, T_BOOKMARK, T_ERROR, T_INVALID };
+
+void append_utf8_codepoint(std::string& o, uint32_t cp) {
+    if (cp < 0x80) {
+        o.push_back((char)cp);
+    } else if (cp < 0x800) {
+        o.push_back((char)(0xC0 | (cp >> 6)));
+        o.push_back((char)(0x80 | (cp & 0x3F)));
+    } else if (cp < 0x10000) {
+        o.push_back((char)(0xE0 | (cp >> 12)));
+        o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+        o.push_back((char)(0x80 | (cp & 0x3F)));
+    } else {
+        o.push_back((char)(0xF0 | (cp >> 18)));
+        o.push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
+        o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+        o.push_back((char)(0x80 | (cp & 0x3F)));
+    }
+}
+
+int hexval(char c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+}
+
+bool read_u4(const char* p, const char* e, uint32_t& out) {
+    if (e - p < 4) return false;
+    uint32_t v = 0;
+    for (int i = 0; i < 4; ++i) {
+        int h = hexval(p[i]);
+        if (h < 0) return false;
+        v = (v << 4) | (uint32_t)h;
+    }
+    out = v;
+    return true;
+}
+
+// JSON string token → Python str; non-string / absent → None (new reference).
+PyObject* span_to_str(const Span& s) {
+    if (!s.is_string()) Py_RETURN_NONE;
+    const char* p = s.p + 1;
+    size_t n = s.n - 2;
+    if (!std::memchr(p, '\\', n)) return PyUnicode_DecodeUTF8(p, (Py_ssize_t)n, "replace");
+    std::string o;
+    o.reserve(n);
+    const char* e = p + n;
+    while (p < e) {
+        char c = *p++;
+        if (c != '\\') {
+            o.push_back(c);
+            continue;
+        }
+        if (p >= e) break;
+        char d = *p++;
+        switch (d) {
+            case '"': o.push_back('"'); break;
+            case '\\': o.push_back('\\'); break;
+            case '/': o.push_back('/'); break;
+            case 'b': o.push_back('\b'); break;
+            case 'f': o.push_back('\f'); break;
+            case 'n': o.push_back('\n'); break;
+            case 'r': o.push_back('\r'); break;
+            case 't': o.push_back('\t'); break;
+            case 'u': {
+                uint32_t cp;
+                if (!read_u4(p, e, cp)) { o.push_back('?'); break; }
+                p += 4;
+                if (cp >= 0xD800 && cp <= 0xDBFF && e - p >= 6 && p[0] == '\\' && p[1] == 'u') {
+                    uint32_t lo;
+                    if (read_u4(p + 2, e, lo) && lo >= 0xDC00 && lo <= 0xDFFF) {
+                        cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+                        p += 6;
+                    }
+                }
+                append_utf8_codepoint(o, cp);
+                break;
+            }
+            default: o.push_back(d);
+        }
+    }
+    return PyUnicode_DecodeUTF8(o.data(), (Py_ssize_t)o.size(), "surrogatepass");
+}
+
+struct InternTable {
+    std::unordered_map<std::string, PyObject*> map;
+    ~InternTable() {
+        for (auto& kv : map) Py_XDECREF(kv.second);
+    }
+    // Small-cardinality strings (namespaces, phases): reuse one object.
+    PyObject* get(const Span& s) {
+        if (!s.is_string() || s.n > 66 || std::memchr(s.p, '\\', s.n)) return span_to_str(s);
+        std::string key(s.p + 1, s.n - 2);
+        auto it = map.find(key);
+        if (it != map.end()) {
+            Py_INCREF(it->second);
+            return it->second;
+        }
+        PyObject* v = span_to_str(s);
+        if (!v) return nullptr;
+        if (map.size() < 4096) {
+            Py_INCREF(v);
+            map.emplace(std::move(key), v);
+        }
+        return v;
+    }
+};
+
+struct DecoderObject {
+    PyObject_HEAD
+    std::string* partial;
+    std::string* env_json;
+    std::string* out;
+    PodSpans* spans;
+    InternTable* interned;
+    long long n_events;
+    long long n_bytes;
+};
+
+PyObject* make_invalid(const char* why, const char* line, size_t n) {
+    PyObject* msg = PyUnicode_FromFormat("%s: %.200s", why, std::string(line, n < 200 ? n : 200).c_str());
+    if (!msg) {
+        PyErr_Clear();
+        msg = PyUnicode_FromString(why);
+    }
+    PyObject* t = PyTuple_New(9);
+    Py_INCREF(g_types[T_INVALID]);
+    PyTuple_SET_ITEM(t, 0, g_types[T_INVALID]);
+    for (int i = 1; i < 8; ++i) {
+        PyObject* v = (i == 6) ? Py_False : Py_None;
+        Py_INCREF(v);
+        PyTuple_SET_ITEM(t, i, v);
+    }
+    PyTuple_SET_ITEM(t, 8, msg);
+    return t;
+}
+
+int type_index(const Span& s) {
+    if (!s.is_string()) return -1;
+    const char* p = s.p + 1;
+    size_t n = s.n - 2;
+    if (n == 5 && !std::memcmp(p, "ADDED", 5)) return T_ADDED;
+    if (n == 8 && !std::memcmp(p, "MODIFIED", 8)) return T_MODIFIED;
+    if (n == 7 && !std::memcmp(p, "DELETED", 7)) return T_DELETED;
+    if (n == 8 && !std::memcmp(p, "BOOKMARK", 8)) return T_BOOKMARK;
+    if (n == 5 && !std::memcmp(p, "ERROR", 5)) return T_ERROR;
+    return -2;  // unknown type string
+}
+
+// Build the event tuple for a parsed pod. `tidx` is the event type index.
+PyObject* event_tuple(DecoderObject* self, int tidx, PyObject* type_obj, const Span& obj_span) {
+    PodSpans& S = *self->spans;
+    PyObject* t = PyTuple_New(9);
+    if (!t) return nullptr;
+    Py_INCREF(type_obj);
+    PyTuple_SET_ITEM(t, 0, type_obj);
+    if (tidx == T_ERROR) {
+        for (int i = 1; i < 8; ++i) {
+            PyObject* v = (i == 6) ? Py_False : Py_None;
+            Py_INCREF(v);
+            PyTuple_SET_ITEM(t, i, v);
+        }
+        PyObject* raw = PyBytes_FromStringAndSize(obj_span.p, (Py_ssize_t)obj_span.n);
+        PyObject* st = raw ? PyObject_CallOneArg(g_json_loads, raw) : nullptr;
+        Py_XDECREF(raw);
+        if (!st) {
+            PyErr_Clear();
+            st = PyDict_New();
+        }
+        PyTuple_SET_ITEM(t, 8, st);
+        return t;
+    }
+    PyObject* uid = span_to_str(S.uid);
+    PyObject* ns = self->interned->get(S.ns);
+    PyObject* name = span_to_str(S.name);
+    PyObject* rv = span_to_str(S.rv);
+    PyObject* phase = S.status_present ? self->interned->get(S.phase) : (Py_INCREF(Py_None), Py_None);
+    if (!uid || !ns || !name || !rv || !phase) {
+        Py_XDECREF(uid); Py_XDECREF(ns); Py_XDECREF(name); Py_XDECREF(rv); Py_XDECREF(phase);
+        Py_DECREF(t);
+        return nullptr;
+    }
+    PyTuple_SET_ITEM(t, 1, uid);
+    PyTuple_SET_ITEM(t, 2, ns);
+    PyTuple_SET_ITEM(t, 3, name);
+    PyTuple_SET_ITEM(t, 4, rv);
+    PyTuple_SET_ITEM(t, 5, phase);
+    PyObject* hs = S.status_present ? Py_True : Py_False;
+    Py_INCREF(hs);
+    PyTuple_SET_ITEM(t, 6, hs);
+    if (tidx == T_BOOKMARK || tidx < 0) {
+        Py_INCREF(Py_None);
+        PyTuple_SET_ITEM(t, 7, Py_None);
+    } else {
+        build_core(*self->out, S, *self->env_json);
+        PyObject* core = PyBytes_FromStringAndSize(self->out->data(), (Py_ssize_t)self->out->size());
+        if (!core) {
+            Py_DECREF(t);
+            return nullptr;
+        }
+        PyTuple_SET_ITEM(t, 7, core);
+    }
+    Py_INCREF(Py_None);
+    PyTuple_SET_ITEM(t, 8, Py_None);
+    return t;
+}
+
+// Decode one watch line. Returns a new tuple, or nullptr with a Python error set.
+PyObject* decode_line(DecoderObject* self, const char* b, size_t n) {
+    PodSpans& S = *self->spans;
+    S.clear();
+    Span type_span, obj_span;
+    try {
+        Parser P(b, b + n);
+        P.object([&](const char* k, size_t kn) {
+            if (KEYIS("type")) {
+                type_span = P.value();
+            } else if (KEYIS("object")) {
+                if (P.peek() != '{') throw ParseError{"object is not a JSON object"};
+                const char* start = P.p_;
+                parse_pod(P, S);
+                obj_span.p = start;
+                obj_span.n = (size_t)(P.p_ - start);
+            } else {
+                P.value();
+            }
+        });
+        P.ws();
+        if (P.p_ != P.end_) throw ParseError{"trailing data"};
+    } catch (const ParseError& e) {
+        return make_invalid(e.msg, b, n);
+    }
+    int tidx = type_index(type_span);
+    if (tidx == -1 || !obj_span.present()) return make_invalid("missing type or object", b, n);
+    PyObject* type_obj;
+    if (tidx >= 0) {
+        type_obj = g_types[tidx];
+        Py_INCREF(type_obj);
+    } else {
+        type_obj = span_to_str(type_span);
+        if (!type_obj) return nullptr;
+    }
+    PyObject* t = event_tuple(self, tidx, type_obj, obj_span);
+    Py_DECREF(type_obj);
+    self->n_events++;
+    return t;
+}
+
+// ----------------------------------------------------------------------------- methods
+
+int Decoder_init(DecoderObject* self, PyObject* args, PyObject* kwds) {
+    static const char* kwlist[] = {"environment", "state_format", nullptr};
+    const char* env = nullptr;
+    Py_ssize_t envn = 0;
+    const char* sf = "structured";
+    if (!PyArg_ParseTupleAndKeywords(args, kwds, "s#|s", (char**)kwlist, &env, &envn, &sf)) return -1;
+    if (std::strcmp(sf, "structured") != 0) {
+        PyErr_SetString(PyExc_ValueError, "native decoder supports state_format='structured' only");
+        return -1;
+    }
+    // environment as a JSON string literal (via json.dumps for exact escaping)
+    PyObject* envs = PyUnicode_FromStringAndSize(env, envn);
+    if (!envs) return -1;
+    PyObject* mod = PyImport_ImportModule("json");
+    PyObject* dumped = mod ? PyObject_CallMethod(mod, "dumps", "O", envs) : nullptr;
+    Py_XDECREF(mod);
+    Py_DECREF(envs);
+    if (!dumped) return -1;
+    Py_ssize_t dn;
+    const char* d = PyUnicode_AsUTF8AndSize(dumped, &dn);
+    if (!d) {
+        Py_DECREF(dumped);
+        return -1;
+    }
+    self->env_json->assign(d, (size_t)dn);
+    Py_DECREF(dumped);
+    return 0;
+}
+
+PyObject* Decoder_new(PyTypeObject* type, PyObject*, PyObject*) {
+    DecoderObject* self = (DecoderObject*)type->tp_alloc(type, 0);
+    if (!self) return nullptr;
+    self->partial = new std::string();
+    self->env_json = new std::string("\"\"");
+    self->out = new std::string();
+    self->out->reserve(8192);
+    self->spans = new PodSpans();
+    self->interned = new InternTable();
+    self->n_events = 0;
+    self->n_bytes = 0;
+    return (PyObject*)self;
+}
+
+void Decoder_dealloc(DecoderObject* self) {
+    delete self->partial;
+    delete self->env_json;
+    delete self->out;
+    delete self->spans;
+    delete self->interned;
+    Py_TYPE(self)->tp_free((PyObject*)self);
+}
+
+bool blank(const char* b, size_t n) {
+    for (size_t i = 0; i < n; ++i)
+        if (!(b[i] == ' ' || b[i] == '\r' || b[i] == '\t' || b[i] == '\n')) return false;
+    return true;
+}
+
+PyObject* Decoder_feed(DecoderObject* self, PyObject* arg) {
+    Py_buffer view;
+    if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) < 0) return nullptr;
+    const char* data = (const char*)view.buf;
+    size_t n = (size_t)view.len;
+    self->n_bytes += (long long)n;
+    PyObject* out = PyList_New(0);
+    if (!out) {
+        PyBuffer_Release(&view);
+        return nullptr;
+    }
+    std::string& partial = *self->partial;
+    size_t pos = 0;
+    bool ok = true;
+    auto emit = [&](const char* b, size_t len) -> bool {
+        if (len == 0 || blank(b, len)) return true;
+        PyObject* t = decode_line(self, b, len);
+        if (!t) return false;
+        int r = PyList_Append(out, t);
+        Py_DECREF(t);
+        return r == 0;
+    };
+    if (!partial.empty()) {
+        const char* nl = (const char*)std::memchr(data, '\n', n);
+        if (!nl) {
+            partial.append(data, n);
+            PyBuffer_Release(&view);
+            return out;
+        }
+        partial.append(data, (size_t)(nl - data));
+        ok = emit(partial.data(), partial.size());
+        partial.clear();
+        pos = (size_t)(nl - data) + 1;
+    }
+    while (ok && pos < n) {
+        const char* nl = (const char*)std::memchr(data + pos, '\n', n - pos);
+        if (!nl) {
+            partial.assign(data + pos, n - pos);
+            break;
+        }
+        ok = emit(data + pos, (size_t)(nl - (data + pos)));
+        pos = (size_t)(nl - data) + 1;
+    }
+    PyBuffer_Release(&view);
+    if (!ok) {
+        Py_DECREF(out);
+        return nullptr;
+    }
+    return out;
+}
+
+PyObject* Decoder_reset(DecoderObject* self, PyObject*) {
+    self->partial->clear();
+    Py_RETURN_NONE;
+}
+
+// decode_list(body) -> (resourceVersion, continue, [ADDED tuples])
+PyObject* Decoder_decode_list(DecoderObject* self, PyObject* arg) {
+    Py_buffer view;
+    if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) < 0) return nullptr;
+    const char* b = (const char*)view.buf;
+    size_t n = (size_t)view.len;
+    PyObject* items = PyList_New(0);
+    Span rv, cont;
+    bool failed = false;
+    try {
+        Parser P(b, b + n);
+        P.object([&](const char* k, size_t kn) {
+            if (KEYIS("metadata")) {
+                if (P.null_here()) return;
+                P.object([&](const char* k2, size_t kn2) {
+                    const char* k = k2; size_t kn = kn2;
+                    if (KEYIS("resourceVersion")) rv = P.value();
+                    else if (KEYIS("continue")) cont = P.value();
+                    else P.value();
+                });
+            } else if (KEYIS("items")) {
+                if (P.null_here()) return;
+                P.array([&]() {
+                    if (failed) { P.value(); return; }
+                    if (P.peek() != '{') { P.value(); return; }
+                    self->spans->clear();
+                    const char* start = P.p_;
+                    parse_pod(P, *self->spans);
+                    Span obj;
+                    obj.p = start;
+                    obj.n = (size_t)(P.p_ - start);
+                    PyObject* t = event_tuple(self, T_ADDED, g_types[T_ADDED], obj);
+                    if (!t || PyList_Append(items, t) < 0) failed = true;
+                    Py_XDECREF(t);
+                    self->n_events++;
+                });
+            } else {
+                P.value();
+            }
+        });
+    } catch (const ParseError& e) {
+        PyBuffer_Release(&view);
+        Py_DECREF(items);
+        PyErr_Format(PyExc_ValueError, "invalid list body: %s", e.msg);
+        return nullptr;
+    }
+    PyBuffer_Release(&view);
+    if (failed) {
+        Py_DECREF(items);
+        return nullptr;
+    }
+    PyObject* rvo = span_to_str(rv);
+    PyObject* co = span_to_str(cont);
+    if (co && PyUnicode_Check(co) && PyUnicode_GET_LENGTH(co) == 0) {
+        Py_DECREF(co);
+        Py_INCREF(Py_None);
+        co = Py_None;
+    }
+    PyObject* res = Py_BuildValue("(NNN)", rvo, co, items);
+    return res;
+}
+
+PyObject* Decoder_core(DecoderObject*, PyObject* ev) {
+    if (!PyTuple_Check(ev) || PyTuple_GET_SIZE(ev) < 8) {
+        PyErr_SetString(PyExc_TypeError, "expected an event tuple");
+        return nullptr;
+    }
+    PyObject* c = PyTuple_GET_ITEM(ev, 7);
+    Py_INCREF(c);
+    return c;
+}
+
+// core_from_summary(uid, ns, name, phase) -> bytes: payload core for a pod
+// known only from the cache (synthesised DELETED after a relist).
+PyObject* Decoder_core_from_summary(DecoderObject* self, PyObject* args) {
+    PyObject *uid, *ns, *name, *phase;
+    if (!PyArg_ParseTuple(args, "OOOO", &uid, &ns, &name, &phase)) return nullptr;
+    PyObject* mod = PyImport_ImportModule("json");
+    if (!mod) return nullptr;
+    PyObject* dumps = PyObject_GetAttrString(mod, "dumps");
+    Py_DECREF(mod);
+    if (!dumps) return nullptr;
+    std::string buf[4];
+    PyObject* vals[4] = {uid, ns, name, phase};
+    for (int i = 0; i < 4; ++i) {
+        PyObject* kw = Py_BuildValue("{s:O}", "ensure_ascii", Py_False);
+        PyObject* a = PyTuple_Pack(1, vals[i]);
+        PyObject* r = (kw && a) ? PyObject_Call(dumps, a, kw) : nullptr;
+        Py_XDECREF(kw);
+        Py_XDECREF(a);
+        if (!r) {
+            Py_DECREF(dumps);
+            return nullptr;
+        }
+        Py_ssize_t ln;
+        const char* s = PyUnicode_AsUTF8AndSize(r, &ln);
+        buf[i].assign(s, (size_t)ln);
+        Py_DECREF(r);
+    }
+    Py_DECREF(dumps);
+    PodSpans S;
+    S.meta_present = true;
+    S.uid = Span{buf[0].data(), buf[0].size()};
+    S.ns = Span{buf[1].data(), buf[1].size()};
+    S.name = Span{buf[2].data(), buf[2].size()};
+    if (phase != Py_None) {
+        S.status_present = true;
+        S.phase = Span{buf[3].data(), buf[3].size()};
+    }
+    build_core(*self->out, S, *self->env_json);
+    return PyBytes_FromStringAndSize(self->out->data(), (Py_ssize_t)self->out->size());
+}
+
+PyObject* Decoder_stats(DecoderObject* self, PyObject*) {
+    return Py_BuildValue("{s:L,s:L}", "events", self->n_events, "bytes", self->n_bytes);
+}
+
+PyMethodDef Decoder_methods[] = {
+    {"feed", (PyCFunction)Decoder_feed, METH_O, "feed(bytes) -> list of event tuples"},
+    {"reset", (PyCFunction)Decoder_reset, METH_NOARGS, "drop any partial line"},
+    {"decode_list", (PyCFunction)Decoder_decode_list, METH_O, "decode_list(body) -> (rv, continue, events)"},
+    {"core", (PyCFunction)Decoder_core, METH_O, "core(event) -> payload core bytes"},
+    {"core_from_summary", (PyCFunction)Decoder_core_from_summary, METH_VARARGS,
+     "core_from_summary(uid, ns, name, phase) -> bytes"},
+    {"stats", (PyCFunction)Decoder_stats, METH_NOARGS, "counters"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyTypeObject DecoderType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+// format_event_timestamp(utc: bool) -> str: datetime.now().isoformat() equivalent
+PyObject* kw_event_timestamp(PyObject*, PyObject* arg) {
+    int utc = PyObject_IsTrue(arg);
+    struct timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    struct tm tmv;
+    time_t secs = ts.tv_sec;
+    if (utc) gmtime_r(&secs, &tmv); else localtime_r(&secs, &tmv);
+    long micro = ts.tv_nsec / 1000;
+    char buf[64];
+    int n = std::snprintf(buf, sizeof buf, "%04d-%02d-%02dT%02d:%02d:%02d", tmv.tm_year + 1900, tmv.tm_mon + 1,
+                          tmv.tm_mday, tmv.tm_hour, tmv.tm_min, tmv.tm_sec);
+    if (micro) n += std::snprintf(buf + n, sizeof buf - n, ".%06ld", micro);
+    if (utc) n += std::snprintf(buf + n, sizeof buf - n, "+00:00");
+    return PyUnicode_FromStringAndSize(buf, n);
+}
+
+PyObject* kw_cpu_features(PyObject*, PyObject*) {
+#if defined(__x86_64__)
+    return Py_BuildValue("{s:O}", "avx2", Parser::use_avx2 ? Py_True : Py_False);
+#else
+    return Py_BuildValue("{s:O}", "avx2", Py_False);
+#endif
+}
+
+PyObject* kw_set_simd(PyObject*, PyObject* arg) {
+#if defined(__x86_64__)
+    int on = PyObject_IsTrue(arg);
+    Parser::use_avx2 = on && __builtin_cpu_supports("avx2");
+#endif
+    Py_RETURN_NONE;
+}
+
+PyMethodDef module_methods[] = {
+    {"event_timestamp", (PyCFunction)kw_event_timestamp, METH_O, "event_timestamp(utc) -> str"},
+    {"cpu_features", (PyCFunction)kw_cpu_features, METH_NOARGS, "SIMD paths in use"},
+    {"set_simd", (PyCFunction)kw_set_simd, METH_O, "enable/disable the AVX2 scanner"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyModuleDef moddef = {PyModuleDef_HEAD_INIT, "_kwcore", "native watch-event decoder", -1, module_methods};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__kwcore(void) {
+    DecoderType.tp_name = "_kwcore.StreamDecoder";
+    DecoderType.tp_basicsize = sizeof(DecoderObject);
+    DecoderType.tp_flags = Py_TPFLAGS_DEFAULT;
+    DecoderType.tp_doc = "StreamDecoder(environment, state_format='structured')";
+    DecoderType.tp_methods = Decoder_methods;
+    DecoderType.tp_new = Decoder_new;
+    DecoderType.tp_init = (initproc)Decoder_init;
+    DecoderType.tp_dealloc = (destructor)Decoder_dealloc;
+    if (PyType_Ready(&DecoderType) < 0) return nullptr;
+    PyObject* m = PyModule_Create(&moddef);
+    if (!m) return nullptr;
+    Py_INCREF(&DecoderType);
+    PyModule_AddObject(m, "StreamDecoder", (PyObject*)&DecoderType);
+    const char* names[6] = {"ADDED", "MODIFIED", "DELETED", "BOOKMARK", "ERROR", "INVALID"};
+    for (int i = 0; i < 6; ++i) {
+        g_types[i] = PyUnicode_InternFromString(names[i]);
+        if (!g_types[i]) return nullptr;
+    }
+    PyObject* json = PyImport_ImportModule("json");
+    if (!json) return nullptr;
+    g_json_loads = PyObject_GetAttrString(json, "loads");
+    Py_DECREF(json);
+    if (!g_json_loads) return nullptr;
+#if defined(__x86_64__)
+    __builtin_cpu_init();
+    Parser::use_avx2 = __builtin_cpu_supports("avx2");
+#endif
+    return m;
+}

@@ -1,0 +1,101 @@
+"""Watch-stream decoding: NDJSON bytes → compact event tuples.
+
+This is the per-event hot path the reference pays inside the ``kubernetes``
+library (line iteration, ``json.loads``, reflective ``V1Pod`` deserialisation;
+SURVEY §3.2 "Hot loop"). Two engines share one interface:
+
+* :class:`PyDecoder` — stdlib ``json`` + :mod:`..models.payload`; the
+  semantic reference for the native engine and the fallback for
+  ``state_format: python_repr``.
+* ``NativeDecoder`` (:mod:`.native`) — C++ single-pass extractor
+  (``ops/csrc/kwcore.cpp``) that never builds Python objects for the pod body
+  and emits the payload core bytes directly.
+
+Event tuple layout (index constants below)::
+
+    (type, uid, namespace, name, resourceVersion, phase, has_status, obj, extra)
+
+``obj`` is the pod dict (Python engine) or the payload core bytes (native);
+call ``decoder.core(ev)`` to get core bytes either way. ``extra`` carries the
+``Status`` dict of an ``ERROR`` event or the error text of an ``INVALID`` line.
+"""
+
+from __future__ import annotations
+
+import json
+from typing import Any, Dict, List, Optional, Tuple
+
+from ..models.payload import build_core
+
+E_TYPE, E_UID, E_NS, E_NAME, E_RV, E_PHASE, E_HAS_STATUS, E_OBJ, E_EXTRA = range(9)
+
+ADDED, MODIFIED, DELETED, BOOKMARK, ERROR, INVALID = (
+    "ADDED", "MODIFIED", "DELETED", "BOOKMARK", "ERROR", "INVALID")
+
+
+def event_from_object(etype: str, obj: Dict[str, Any]) -> tuple:
+    if etype == ERROR:
+        return (ERROR, None, None, None, None, None, False, None, obj)
+    md = obj.get("metadata") or {}
+    st = obj.get("status")
+    return (etype, md.get("uid"), md.get("namespace"), md.get("name"), md.get("resourceVersion"),
+            st.get("phase") if st is not None else None, st is not None, obj, None)
+
+
+class PyDecoder:
+    name = "python"
+
+    def __init__(self, environment: str, state_format: str = "structured") -> None:
+        self.environment = environment
+        self.state_format = state_format
+        self._partial = b""
+
+    def reset(self) -> None:
+        self._partial = b""
+
+    def feed(self, data: bytes) -> List[tuple]:
+        buf = self._partial + data if self._partial else data
+        lines = buf.split(b"\n")
+        self._partial = lines.pop()
+        out = []
+        for line in lines:
+            if not line.strip():
+                continue
+            out.append(self.decode_line(line))
+        return out
+
+    def decode_line(self, line: bytes) -> tuple:
+        try:
+            doc = json.loads(line)
+            etype = doc["type"]
+            obj = doc["object"]
+            if not isinstance(obj, dict):
+                raise ValueError("object is not a JSON object")
+        except (ValueError, KeyError, TypeError) as exc:
+            return (INVALID, None, None, None, None, None, False, None, f"{exc}: {line[:200]!r}")
+        return event_from_object(etype, obj)
+
+    def decode_list(self, body: bytes) -> Tuple[Optional[str], Optional[str], List[tuple]]:
+        doc = json.loads(body)
+        md = doc.get("metadata") or {}
+        items = doc.get("items") or []
+        return (md.get("resourceVersion"), md.get("continue") or None,
+                [event_from_object(ADDED, it) for it in items])
+
+    def core(self, ev: tuple) -> bytes:
+        return build_core(ev[E_OBJ], self.environment, self.state_format)
+
+    def core_from_summary(self, uid: str, ns: Optional[str], name: Optional[str],
+                          phase: Optional[str]) -> bytes:
+        pod = {"metadata": {"uid": uid, "namespace": ns, "name": name}}
+        if phase is not None:
+            pod["status"] = {"phase": phase}
+        return build_core(pod, self.environment, self.state_format)
+
+
+def make_decoder(engine: str, environment: str, state_format: str = "structured"):
+    """``engine="native"`` requires the C++ extension and raises if it is missing."""
+    if engine == "python" or state_format == "python_repr":
+        return PyDecoder(environment, state_format)
+    from .native import NativeDecoder
+    return NativeDecoder(environment, state_format)

@@ -1,0 +1,113 @@
+"""Loader and build driver for the native decoder extension ``_kwcore``.
+
+The extension (``ops/csrc/kwcore.cpp``) is compiled in-tree with the host C++
+compiler into ``k8s_watcher_amd/ops/_kwcore<EXT_SUFFIX>`` — by
+``__graft_entry__.build()``, ``python -m k8s_watcher_amd.ops.native``, or
+lazily by the test session. ``watcher.engine: native`` (the default) requires
+it: :class:`NativeDecoder` raises :class:`NativeUnavailable` instead of
+silently falling back to the Python engine.
+"""
+
+from __future__ import annotations
+
+import importlib
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "csrc", "kwcore.cpp")
+SO = os.path.join(HERE, "_kwcore" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+
+
+class NativeUnavailable(ImportError):
+    """The C++ extension is not built (run ``python -m k8s_watcher_amd.ops.native``)."""
+
+
+def compiler() -> str:
+    for cand in (os.environ.get("CXX"), "g++", "c++", "clang++"):
+        if cand and shutil.which(cand):
+            return cand
+    raise NativeUnavailable("no C++ compiler found (set $CXX)")
+
+
+def build_command() -> list:
+    inc = sysconfig.get_paths()["include"]
+    return [compiler(), "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
+            "-fno-strict-aliasing", "-Wall", "-Wno-shadow", "-Wno-unused-function",
+            f"-I{inc}", SRC, "-o", SO]
+
+
+def is_fresh() -> bool:
+    return os.path.exists(SO) and os.path.getmtime(SO) >= os.path.getmtime(SRC)
+
+
+def build(quiet: bool = False) -> str:
+    cmd = build_command()
+    tmp = SO + ".tmp"
+    cmd[-1] = tmp
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise NativeUnavailable(f"building _kwcore failed:\n{' '.join(cmd)}\n{res.stderr}")
+    os.replace(tmp, SO)
+    if not quiet:
+        print(f"built {SO}")
+    return SO
+
+
+def ensure_built(quiet: bool = True) -> str:
+    if not is_fresh():
+        build(quiet)
+    return SO
+
+
+_mod = None
+
+
+def load():
+    global _mod
+    if _mod is None:
+        try:
+            _mod = importlib.import_module("k8s_watcher_amd.ops._kwcore")
+        except ImportError as exc:
+            raise NativeUnavailable(
+                f"native engine requested but {os.path.basename(SO)} is not built ({exc}); "
+                "run `python -m k8s_watcher_amd.ops.native` or set watcher.engine: python") from None
+    return _mod
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except NativeUnavailable:
+        return False
+
+
+class NativeDecoder:
+    """Same interface as :class:`..decode.PyDecoder`, backed by ``_kwcore.StreamDecoder``."""
+
+    name = "native"
+
+    def __init__(self, environment: str, state_format: str = "structured") -> None:
+        mod = load()
+        d = mod.StreamDecoder(environment, state_format)
+        self._d = d
+        self.environment = environment
+        self.state_format = state_format
+        # bind C methods directly: no Python frame per call
+        self.feed = d.feed
+        self.reset = d.reset
+        self.decode_list = d.decode_list
+        self.core = d.core
+        self.core_from_summary = d.core_from_summary
+        self.stats = d.stats
+
+
+if __name__ == "__main__":
+    build(quiet=False)
+    mod = load()
+    print("loaded", mod.__file__, mod.cpu_features())
+    sys.exit(0)

@@ -1,0 +1,421 @@
+"""Asynchronous clusterapi notifier pool (SURVEY C11 + §7.1 step 5).
+
+Reference: ``ClusterApiClient.update_pod_status`` does one blocking
+``requests`` POST per event with no timeout and no retry, and counts only
+HTTP 200 as success (``/root/reference/watcher/clusterapi_client.py:20-53``);
+had it been enabled, every event would have stalled the watch stream for a
+full round trip.
+
+This pool keeps ``connections`` keep-alive HTTP/1.1 connections to
+clusterapi, each carrying up to ``pipeline_depth`` requests in flight, all
+driven from the event-loop thread:
+
+* **Per-pod ordering** — a pod's notifications always use the same
+  connection (``hash(uid) % connections``), whose requests are sent and
+  answered in FIFO order; different pods proceed in parallel.
+* **Monotonic delivery under failure** — a failed request is retried (after
+  ``clusterapi.retry`` backoff) only while it is still the newest
+  notification for its pod; once a newer one exists the stale one is dropped
+  as *superseded*, so a retry can never overwrite newer state.
+  Delivery is at-least-once.
+* **Success** is any 2xx (reference: exactly 200). 408/429/5xx and transport
+  errors are retried; other statuses fail at once.
+* **Timeout** — ``clusterapi.timeout`` is enforced per request by a
+  watchdog that aborts a connection whose oldest request is overdue.
+* **Backpressure** — past ``queue_size`` outstanding requests the pool
+  reports saturation and the watch reader pauses its socket until half
+  the queue has drained; optional latest-state *coalescing* replaces a
+  pod's not-yet-sent body instead of queueing another one.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import collections
+import logging
+import time
+import zlib
+from typing import Callable, Deque, Dict, List, Optional
+from urllib.parse import urlsplit
+
+from ..metrics import Metrics
+from ..models.payload import finish_body
+from ..net.http import ResponseParser
+from ..utils.backoff import Backoff
+from ..utils.config import ClusterApiSettings, RetryPolicy
+from ..utils.logsetup import NOTIFIER_LOGGER, SERVICE_LOGGER
+from ..utils.aio import with_timeout
+
+RETRYABLE_STATUS = frozenset({408, 425, 429, 500, 502, 503, 504})
+
+
+class NotifyRequest:
+    __slots__ = ("uid", "seq", "etype", "ns", "name", "body", "read_ns", "attempts", "sent_ns", "conn")
+
+    def __init__(self, uid, seq, etype, ns, name, body, read_ns, conn):
+        self.uid = uid
+        self.seq = seq
+        self.etype = etype
+        self.ns = ns
+        self.name = name
+        self.body = body
+        self.read_ns = read_ns
+        self.attempts = 0
+        self.sent_ns = 0
+        self.conn = conn
+
+
+class _Conn(asyncio.Protocol):
+    """One pooled connection. Requests are written in order; responses matched FIFO."""
+
+    IDLE, CONNECTING, UP = range(3)
+
+    def __init__(self, pool: "NotifierPool", index: int) -> None:
+        self.pool = pool
+        self.index = index
+        self.state = self.IDLE
+        self.transport: Optional[asyncio.Transport] = None
+        self.queue: Deque[NotifyRequest] = collections.deque()
+        self.inflight: Deque[NotifyRequest] = collections.deque()
+        self.parser = ResponseParser()
+        self._arm_parser()
+        self.connect_backoff = Backoff(RetryPolicy(1_000_000, 0.05, 2.0, 5.0, 0.2))
+        self.reconnect_handle: Optional[asyncio.TimerHandle] = None
+
+    def _arm_parser(self) -> None:
+        p = self.parser
+        p.reset()
+        p.on_complete = self._on_message
+
+    # ------------------------------------------------------------- asyncio protocol
+    def connection_made(self, transport) -> None:  # type: ignore[override]
+        self.transport = transport
+        self.state = self.UP
+        self.connect_backoff.reset()
+        self._arm_parser()
+        self.pump()
+
+    def data_received(self, data: bytes) -> None:  # type: ignore[override]
+        parser = self.parser
+        try:
+            while data:
+                data = parser.feed(data)
+                if parser.state == ResponseParser.DONE:
+                    self._arm_parser()
+        except Exception as exc:  # noqa: BLE001 - protocol violation: drop the connection
+            self.pool.log.error(f"Unexpected error calling clusterapi: {exc}")
+            if self.transport is not None:
+                self.transport.abort()
+            return
+        self.pump()
+
+    def connection_lost(self, exc) -> None:  # type: ignore[override]
+        self.transport = None
+        self.state = self.IDLE
+        failed = list(self.inflight)
+        self.inflight.clear()
+        reason = f"Connection error: Unable to connect to clusterapi at {self.pool.endpoint_url}"
+        for req in failed:
+            self.pool._failed(req, None, reason)
+        if self.queue:
+            self.schedule_connect()
+
+    # ------------------------------------------------------------- internals
+    def _on_message(self, p: ResponseParser) -> None:
+        if not self.inflight:
+            return  # unsolicited response; ignore
+        req = self.inflight.popleft()
+        status = p.status
+        if 200 <= status < 300:
+            self.pool._delivered(req)
+        else:
+            self.pool._failed(req, status, p.body().decode("utf-8", "replace")[:500])
+        if not p.keep_alive and self.transport is not None:
+            self.transport.close()
+
+    def schedule_connect(self) -> None:
+        if self.state != self.IDLE or self.reconnect_handle is not None or self.pool.closing:
+            return
+        delay = 0.0 if self.connect_backoff.attempt == 0 else self.connect_backoff.next_delay()
+        if self.connect_backoff.attempt == 0:
+            self.connect_backoff.attempt = 1
+        self.reconnect_handle = self.pool.loop.call_later(delay, self._start_connect)
+
+    def _start_connect(self) -> None:
+        self.reconnect_handle = None
+        if self.state != self.IDLE or self.pool.closing:
+            return
+        self.state = self.CONNECTING
+        self.pool.loop.create_task(self._connect())
+
+    async def _connect(self) -> None:
+        pool = self.pool
+        try:
+            await with_timeout(
+                pool.loop.create_connection(lambda: self, pool.host, pool.port, ssl=pool.ssl_context,
+                                            server_hostname=pool.host if pool.ssl_context else None),
+                pool.settings.timeout)
+        except (OSError, asyncio.TimeoutError) as exc:
+            self.state = self.IDLE
+            failed = list(self.queue)
+            self.queue.clear()
+            for req in failed:
+                pool._failed(req, None, f"Connection error: Unable to connect to clusterapi at "
+                                        f"{pool.endpoint_url} ({exc.__class__.__name__})")
+            if self.queue:
+                self.schedule_connect()
+
+    def pump(self) -> None:
+        """Move queued requests onto the wire up to the pipeline depth."""
+        if self.state != self.UP:
+            if self.queue:
+                self.schedule_connect()
+            return
+        depth = self.pool.depth
+        inflight = self.inflight
+        queue = self.queue
+        if not queue or len(inflight) >= depth:
+            return
+        parts: List[bytes] = []
+        now = time.monotonic_ns()
+        head = self.pool.request_head
+        unsent = self.pool.unsent
+        while queue and len(inflight) < depth:
+            req = queue.popleft()
+            if unsent.get(req.uid) is req:
+                del unsent[req.uid]
+            req.sent_ns = now
+            req.attempts += 1
+            inflight.append(req)
+            parts.append(head)
+            parts.append(str(len(req.body)).encode())
+            parts.append(b"\r\n\r\n")
+            parts.append(req.body)
+        assert self.transport is not None
+        self.transport.write(b"".join(parts))
+
+
+class NotifierPool:
+    """See module docstring. Create inside a running event loop."""
+
+    def __init__(self, settings: ClusterApiSettings, metrics: Optional[Metrics] = None,
+                 ts_mode: str = "local", log_events: bool = False, ssl_context=None,
+                 on_saturation: Optional[Callable[[bool], None]] = None) -> None:
+        self.settings = settings
+        self.metrics = metrics or Metrics()
+        self.loop = asyncio.get_running_loop()
+        self.log = logging.getLogger(NOTIFIER_LOGGER)
+        self.svc_log = logging.getLogger(SERVICE_LOGGER)
+        self.log_events = log_events
+        self.ts_mode = ts_mode
+        u = urlsplit(settings.base_url)
+        self.host = u.hostname or "localhost"
+        self.port = u.port or (443 if u.scheme == "https" else 80)
+        if u.scheme == "https" and ssl_context is None:
+            import ssl
+            ssl_context = ssl.create_default_context(cafile=settings.ca_file)
+            if not settings.verify_tls:
+                ssl_context.check_hostname = False
+                ssl_context.verify_mode = ssl.CERT_NONE
+        self.ssl_context = ssl_context if u.scheme == "https" else None
+        path = (u.path.rstrip("/") + settings.pod_update) or "/"
+        self.endpoint_url = settings.base_url + settings.pod_update
+        default_port = 443 if u.scheme == "https" else 80
+        host_hdr = self.host if self.port == default_port else f"{self.host}:{self.port}"
+        head = (f"POST {path} HTTP/1.1\r\nHost: {host_hdr}\r\nContent-Type: application/json\r\n"
+                f"User-Agent: k8s-watcher-amd/1.0\r\n")
+        if settings.api_key:
+            head += f"Authorization: Bearer {settings.api_key}\r\n"
+        head += "Content-Length: "
+        self.request_head = head.encode("latin-1")
+        self.depth = settings.pool.pipeline_depth
+        self.conns = [_Conn(self, i) for i in range(settings.pool.connections)]
+        self.latest: Dict[str, int] = {}
+        self.unsent: Dict[str, NotifyRequest] = {}
+        self.seq = 0
+        self.pending = 0
+        self.high_water = settings.pool.queue_size
+        self.low_water = max(1, settings.pool.queue_size // 2)
+        self.saturated = False
+        self.on_saturation = on_saturation
+        self.closing = False
+        self._idle_event = asyncio.Event()
+        self._idle_event.set()
+        self._dirty: List[_Conn] = []
+        self.retry_policy = settings.retry
+        self._watchdog = self.loop.create_task(self._watchdog_loop())
+
+    # ------------------------------------------------------------------ public API
+    def submit(self, uid: str, etype: str, ns: Optional[str], name: Optional[str], core: bytes,
+               read_ns: int, ts: str) -> None:
+        """Queue one notification; call :meth:`flush` once per batch to send."""
+        body = finish_body(core, etype, ts)
+        m = self.metrics.c
+        m["notify_submitted"] += 1
+        if self.settings.pool.coalesce:
+            old = self.unsent.get(uid)
+            if old is not None:
+                old.body = body
+                old.etype = etype
+                self.seq += 1
+                old.seq = self.seq
+                self.latest[uid] = old.seq
+                old.read_ns = read_ns
+                m["notify_coalesced"] += 1
+                return
+        self.seq += 1
+        conn = self.conns[zlib.crc32(uid.encode()) % len(self.conns)] if uid else self.conns[0]
+        req = NotifyRequest(uid, self.seq, etype, ns, name, body, read_ns, conn)
+        self.latest[uid] = req.seq
+        self.unsent[uid] = req
+        conn.queue.append(req)
+        if len(conn.queue) == 1 or conn.state != _Conn.UP:
+            self._dirty.append(conn)
+        self._add_pending(1)
+
+    def flush(self) -> None:
+        dirty = self._dirty
+        if not dirty:
+            return
+        self._dirty = []
+        for conn in dirty:
+            conn.pump()
+
+    async def health_check(self, timeout: float = 5.0) -> bool:
+        """``GET <health>``; True on 2xx (reference: ``clusterapi_client.py:55-61``)."""
+        from ..net.http import HttpClient
+        client = HttpClient(self.settings.base_url, self.ssl_context, timeout=timeout)
+        try:
+            resp = await client.request("GET", self.settings.health)
+            return resp.ok
+        except Exception:  # noqa: BLE001 - parity: any failure -> False
+            return False
+        finally:
+            await client.close()
+
+    async def drain(self, timeout: Optional[float] = None) -> bool:
+        self.flush()
+        try:
+            await with_timeout(self._idle_event.wait(), timeout)
+            return True
+        except asyncio.TimeoutError:
+            return False
+
+    async def close(self) -> None:
+        self.closing = True
+        self._watchdog.cancel()
+        for c in self.conns:
+            if c.reconnect_handle is not None:
+                c.reconnect_handle.cancel()
+            if c.transport is not None:
+                c.transport.close()
+        await asyncio.sleep(0)
+
+    def outstanding(self) -> int:
+        return self.pending
+
+    # ------------------------------------------------------------------ bookkeeping
+    def _add_pending(self, n: int) -> None:
+        self.pending += n
+        if self.pending > 0:
+            self._idle_event.clear()
+        else:
+            self._idle_event.set()
+        if not self.saturated and self.pending >= self.high_water:
+            self.saturated = True
+            if self.on_saturation:
+                self.on_saturation(True)
+        elif self.saturated and self.pending <= self.low_water:
+            self.saturated = False
+            if self.on_saturation:
+                self.on_saturation(False)
+
+    def _delivered(self, req: NotifyRequest) -> None:
+        m = self.metrics
+        m.c["notify_delivered"] += 1
+        m.latency.observe_ns(time.monotonic_ns() - req.read_ns)
+        if self.latest.get(req.uid) == req.seq:
+            del self.latest[req.uid]
+        if self.log_events:
+            self.svc_log.info(f"Successfully notified clusterapi about {req.etype} event for {req.ns}/{req.name}")
+        self._add_pending(-1)
+
+    def _failed(self, req: NotifyRequest, status: Optional[int], detail: str) -> None:
+        if status is not None:
+            self.log.error(f"Failed to update pod data. Status: {status}, Response: {detail}")
+        else:
+            self.log.error(detail)
+        retryable = status is None or status in RETRYABLE_STATUS
+        if self.latest.get(req.uid) != req.seq:
+            self.metrics.c["notify_superseded"] += 1
+            self._add_pending(-1)
+            return
+        if retryable and req.attempts < self.retry_policy.max_attempts and not self.closing:
+            self.metrics.c["notify_retried"] += 1
+            delay = self.retry_policy.delay(req.attempts)
+            self.loop.call_later(delay, self._retry_fire, req)
+            return
+        self._give_up(req)
+
+    def _give_up(self, req: NotifyRequest) -> None:
+        self.metrics.c["notify_failed"] += 1
+        if self.latest.get(req.uid) == req.seq:
+            del self.latest[req.uid]
+        self.svc_log.error(f"Failed to notify clusterapi about {req.etype} event for {req.ns}/{req.name}")
+        self._add_pending(-1)
+
+    def _retry_fire(self, req: NotifyRequest) -> None:
+        if self.latest.get(req.uid) != req.seq:
+            self.metrics.c["notify_superseded"] += 1
+            self._add_pending(-1)
+            return
+        if self.closing:
+            self._give_up(req)
+            return
+        conn = req.conn
+        conn.queue.appendleft(req)
+        conn.pump()
+
+    async def _watchdog_loop(self) -> None:
+        timeout_ns = int(self.settings.timeout * 1e9)
+        period = max(0.05, min(1.0, self.settings.timeout / 4))
+        while True:
+            await asyncio.sleep(period)
+            now = time.monotonic_ns()
+            for c in self.conns:
+                if c.inflight and now - c.inflight[0].sent_ns > timeout_ns and c.transport is not None:
+                    self.log.error(f"Timeout error: Request to {self.endpoint_url} timed out")
+                    c.transport.abort()
+
+
+class NullNotifier:
+    """Used when ``clusterapi.enabled: false``: payloads are built and counted, not sent.
+
+    This is the reference as shipped (the POST is commented out,
+    ``pod_watcher.py:236``).
+    """
+
+    def __init__(self, metrics: Optional[Metrics] = None) -> None:
+        self.metrics = metrics or Metrics()
+        self.saturated = False
+
+    def submit(self, uid, etype, ns, name, core, read_ns, ts) -> None:
+        finish_body(core, etype, ts)
+        self.metrics.c["notify_submitted"] += 1
+        self.metrics.c["notify_delivered"] += 1
+        self.metrics.latency.observe_ns(time.monotonic_ns() - read_ns)
+
+    def flush(self) -> None:
+        pass
+
+    async def health_check(self, timeout: float = 5.0) -> bool:
+        return True
+
+    async def drain(self, timeout: Optional[float] = None) -> bool:
+        return True
+
+    async def close(self) -> None:
+        pass
+
+    def outstanding(self) -> int:
+        return 0

@@ -1,0 +1,518 @@
+"""Scriptable fake kube-apiserver (replaces the external mock at ``localhost:9988``).
+
+The reference's only end-to-end path talks to a mock API server that is not
+in the repository (``/root/reference/assets/config:5``,
+``test_k8s_mock.py:37-80``). This module is that server, built to
+be faithful where the watcher's correctness depends on it:
+
+* ``GET /version``, ``GET /api/v1/namespaces`` (``limit``/``continue``);
+* ``GET /api/v1/pods`` and ``/api/v1/namespaces/{ns}/pods`` — paginated LIST
+  (``limit``/``continue``, ``labelSelector`` equality terms, ``fieldSelector``
+  on ``metadata.namespace|name``, ``status.phase``, ``spec.nodeName``);
+* WATCH on the same paths (``watch=true``): no/"0" resourceVersion → synthetic
+  ``ADDED`` for current pods then live events; a resourceVersion → replay of
+  the retained history after it; a compacted version → ``ERROR`` 410 event (or
+  HTTP 410 with ``expired_as_http_status``); ``timeoutSeconds``;
+  ``allowWatchBookmarks`` bookmarks on demand or periodically;
+* one HTTP chunk per event, as the real server flushes;
+* fault injection: drop every connection, expire every watch, fail the next
+  N requests with a status, compact history, bearer-token auth (401).
+
+Runs inside the caller's event loop (``await srv.start()``), in a background
+thread (:class:`ServerThread`), or as a process
+(``python -m k8s_watcher_amd.testing.fake_apiserver --port 9988``).
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import base64
+import collections
+import copy
+import json
+import threading
+import time
+import uuid
+from typing import Any, Deque, Dict, List, Optional, Set, Tuple
+from urllib.parse import parse_qs, urlsplit
+from ..utils.aio import with_timeout
+
+JSON = "application/json"
+
+
+def _chunk(data: bytes) -> bytes:
+    return b"%x\r\n%s\r\n" % (len(data), data)
+
+
+def _status(code: int, reason: str, message: str) -> Dict[str, Any]:
+    return {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Failure",
+            "message": message, "reason": reason, "code": code}
+
+
+def _match_labels(pod: Dict[str, Any], selector: Optional[str]) -> bool:
+    if not selector:
+        return True
+    labels = (pod.get("metadata") or {}).get("labels") or {}
+    for term in selector.split(","):
+        term = term.strip()
+        if not term:
+            continue
+        if "!=" in term:
+            k, v = term.split("!=", 1)
+            if labels.get(k.strip()) == v.strip():
+                return False
+        elif "=" in term:
+            k, v = term.replace("==", "=").split("=", 1)
+            if labels.get(k.strip()) != v.strip():
+                return False
+        elif term.startswith("!"):
+            if term[1:] in labels:
+                return False
+        elif term not in labels:
+            return False
+    return True
+
+
+_FIELD_PATHS = {
+    "metadata.namespace": lambda p: (p.get("metadata") or {}).get("namespace"),
+    "metadata.name": lambda p: (p.get("metadata") or {}).get("name"),
+    "status.phase": lambda p: (p.get("status") or {}).get("phase"),
+    "spec.nodeName": lambda p: (p.get("spec") or {}).get("nodeName"),
+}
+
+
+def _match_fields(pod: Dict[str, Any], selector: Optional[str]) -> bool:
+    if not selector:
+        return True
+    for term in selector.split(","):
+        term = term.strip()
+        if not term:
+            continue
+        neg = "!=" in term
+        k, v = term.split("!=" if neg else "=", 1)
+        k = k.strip().rstrip("=")
+        get = _FIELD_PATHS.get(k)
+        if get is None:
+            continue
+        val = get(pod) or ""
+        if (val == v.strip()) == neg:
+            return False
+    return True
+
+
+class _Watch:
+    __slots__ = ("writer", "namespace", "labels", "fields", "bookmarks", "closed")
+
+    def __init__(self, writer, namespace, labels, fields, bookmarks):
+        self.writer = writer
+        self.namespace = namespace
+        self.labels = labels
+        self.fields = fields
+        self.bookmarks = bookmarks
+        self.closed = asyncio.Event()
+
+    def wants(self, pod: Dict[str, Any]) -> bool:
+        md = pod.get("metadata") or {}
+        if self.namespace and md.get("namespace") != self.namespace:
+            return False
+        return _match_labels(pod, self.labels) and _match_fields(pod, self.fields)
+
+
+class FakeApiServer:
+    def __init__(self, token: Optional[str] = None, history_limit: int = 1_000_000,
+                 namespaces: Optional[List[str]] = None, expired_as_http_status: bool = False,
+                 bookmark_interval: Optional[float] = None, start_rv: int = 1000) -> None:
+        self.token = token
+        self.history_limit = history_limit
+        self.extra_namespaces = list(namespaces or ["default", "kube-system"])
+        self.expired_as_http_status = expired_as_http_status
+        self.bookmark_interval = bookmark_interval
+        self.rv = start_rv
+        self.pods: Dict[Tuple[str, str], Dict[str, Any]] = {}
+        # (rv, namespace, pod-for-filtering, encoded line)
+        self.history: Deque[Tuple[int, str, Dict[str, Any], bytes]] = collections.deque()
+        self.compacted_rv = start_rv
+        self.watches: Set[_Watch] = set()
+        self.writers: Set[asyncio.StreamWriter] = set()
+        self.fail_next: List[Tuple[int, str]] = []
+        self.requests: List[Tuple[str, str]] = []
+        self.server: Optional[asyncio.AbstractServer] = None
+        self.port = 0
+        self.loop: Optional[asyncio.AbstractEventLoop] = None
+        self._bm_task: Optional[asyncio.Task] = None
+
+    # ------------------------------------------------------------------ lifecycle
+    async def start(self, host: str = "127.0.0.1", port: int = 0) -> int:
+        self.loop = asyncio.get_running_loop()
+        self.server = await asyncio.start_server(self._handle, host, port, limit=1 << 20)
+        self.port = self.server.sockets[0].getsockname()[1]
+        if self.bookmark_interval:
+            self._bm_task = asyncio.ensure_future(self._bookmark_loop())
+        return self.port
+
+    @property
+    def url(self) -> str:
+        return f"http://127.0.0.1:{self.port}"
+
+    async def stop(self) -> None:
+        if self._bm_task:
+            self._bm_task.cancel()
+        if self.server is not None:
+            self.server.close()
+        self.drop_connections()
+        if self.server is not None:
+            try:
+                await with_timeout(self.server.wait_closed(), 2)
+            except asyncio.TimeoutError:
+                pass
+
+    async def _bookmark_loop(self) -> None:
+        while True:
+            await asyncio.sleep(self.bookmark_interval or 1.0)
+            self.emit_bookmark()
+
+    # ------------------------------------------------------------------ state mutation
+    def _next_rv(self) -> int:
+        self.rv += 1
+        return self.rv
+
+    def _record(self, etype: str, pod: Dict[str, Any]) -> None:
+        rv = int(pod["metadata"]["resourceVersion"])
+        line = json.dumps({"type": etype, "object": pod}, separators=(",", ":"),
+                          ensure_ascii=False).encode("utf-8") + b"\n"
+        ns = pod["metadata"].get("namespace", "")
+        self.history.append((rv, ns, pod, line))
+        while len(self.history) > self.history_limit:
+            old = self.history.popleft()
+            self.compacted_rv = old[0]
+        data = _chunk(line)
+        for w in list(self.watches):
+            if w.wants(pod):
+                try:
+                    w.writer.write(data)
+                except Exception:  # noqa: BLE001
+                    self.watches.discard(w)
+
+    def create(self, pod: Dict[str, Any]) -> Dict[str, Any]:
+        pod = copy.deepcopy(pod)
+        md = pod.setdefault("metadata", {})
+        md.setdefault("namespace", "default")
+        md.setdefault("uid", str(uuid.uuid4()))
+        md.setdefault("creationTimestamp", time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()))
+        md["resourceVersion"] = str(self._next_rv())
+        self.pods[(md["namespace"], md["name"])] = pod
+        self._record("ADDED", pod)
+        return pod
+
+    def update(self, pod: Dict[str, Any]) -> Dict[str, Any]:
+        pod = copy.deepcopy(pod)
+        md = pod["metadata"]
+        key = (md.get("namespace", "default"), md["name"])
+        if key not in self.pods:
+            return self.create(pod)
+        md["uid"] = self.pods[key]["metadata"]["uid"]
+        md["resourceVersion"] = str(self._next_rv())
+        self.pods[key] = pod
+        self._record("MODIFIED", pod)
+        return pod
+
+    def delete(self, namespace: str, name: str, final: Optional[Dict[str, Any]] = None) -> Optional[Dict]:
+        pod = self.pods.pop((namespace, name), None)
+        if pod is None:
+            return None
+        pod = copy.deepcopy(final if final is not None else pod)
+        pod["metadata"]["uid"] = pod["metadata"].get("uid") or str(uuid.uuid4())
+        pod["metadata"]["resourceVersion"] = str(self._next_rv())
+        self._record("DELETED", pod)
+        return pod
+
+    def apply(self, etype: str, pod: Dict[str, Any]) -> Dict[str, Any]:
+        """Apply a generated ``(type, object)`` event (see :mod:`.podgen`)."""
+        md = pod["metadata"]
+        if etype == "ADDED":
+            return self.create(pod)
+        if etype == "MODIFIED":
+            return self.update(pod)
+        if etype == "DELETED":
+            return self.delete(md.get("namespace", "default"), md["name"], final=pod) or pod
+        raise ValueError(etype)
+
+    def emit_bookmark(self) -> None:
+        for w in list(self.watches):
+            if w.bookmarks:
+                line = json.dumps({"type": "BOOKMARK", "object": {
+                    "kind": "Pod", "apiVersion": "v1",
+                    "metadata": {"resourceVersion": str(self.rv),
+                                 "annotations": {"k8s.io/initial-events-end": "true"}}}},
+                    separators=(",", ":")).encode() + b"\n"
+                w.writer.write(_chunk(line))
+
+    def expire_watches(self) -> None:
+        """Send ``ERROR 410`` to every open watch and end it (etcd compaction)."""
+        line = json.dumps({"type": "ERROR", "object": _status(
+            410, "Expired", "too old resource version")}).encode() + b"\n"
+        for w in list(self.watches):
+            try:
+                w.writer.write(_chunk(line) + b"0\r\n\r\n")
+                w.writer.close()
+            except Exception:  # noqa: BLE001
+                pass
+            w.closed.set()
+        self.watches.clear()
+
+    def compact(self, keep_last: int = 0) -> None:
+        """Forget history so resuming from an older resourceVersion yields 410."""
+        while len(self.history) > keep_last:
+            old = self.history.popleft()
+            self.compacted_rv = old[0]
+        if keep_last == 0:
+            self.compacted_rv = self.rv
+
+    def drop_connections(self) -> None:
+        """Abort every client connection (simulated API-server restart)."""
+        for w in list(self.watches):
+            w.closed.set()
+        self.watches.clear()
+        for wr in list(self.writers):
+            try:
+                wr.transport.abort()
+            except Exception:  # noqa: BLE001
+                pass
+        self.writers.clear()
+
+    def fail_requests(self, n: int, status: int = 500, path_prefix: str = "") -> None:
+        for _ in range(n):
+            self.fail_next.append((status, path_prefix))
+
+    # ------------------------------------------------------------------ HTTP
+    async def _handle(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
+        self.writers.add(writer)
+        try:
+            while True:
+                try:
+                    line = await reader.readline()
+                except (ConnectionError, asyncio.LimitOverrunError):
+                    return
+                if not line:
+                    return
+                headers: Dict[str, str] = {}
+                while True:
+                    h = await reader.readline()
+                    if h in (b"\r\n", b"\n", b""):
+                        break
+                    k, _, v = h.decode("latin-1").partition(":")
+                    headers[k.strip().lower()] = v.strip()
+                n = int(headers.get("content-length", "0") or 0)
+                if n:
+                    await reader.readexactly(n)
+                parts = line.decode("latin-1").split()
+                if len(parts) < 2:
+                    return
+                method, target = parts[0], parts[1]
+                self.requests.append((method, target))
+                keep = await self._route(method, target, headers, writer)
+                if not keep:
+                    return
+        except (ConnectionError, asyncio.IncompleteReadError):
+            return
+        finally:
+            self.writers.discard(writer)
+            try:
+                writer.close()
+            except Exception:  # noqa: BLE001
+                pass
+
+    def _send_json(self, writer, code: int, doc: Any, reason: str = "OK") -> None:
+        body = json.dumps(doc, separators=(",", ":"), ensure_ascii=False).encode("utf-8")
+        writer.write(b"HTTP/1.1 %d %s\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n"
+                     % (code, reason.encode(), len(body)) + body)
+
+    async def _route(self, method: str, target: str, headers: Dict[str, str], writer) -> bool:
+        u = urlsplit(target)
+        q = {k: v[-1] for k, v in parse_qs(u.query, keep_blank_values=True).items()}
+        path = u.path
+        if self.token is not None and headers.get("authorization") != f"Bearer {self.token}":
+            self._send_json(writer, 401, _status(401, "Unauthorized", "Unauthorized"), "Unauthorized")
+            return True
+        if self.fail_next:
+            st, prefix = self.fail_next[0]
+            if path.startswith(prefix):
+                self.fail_next.pop(0)
+                self._send_json(writer, st, _status(st, "InternalError", "injected failure"), "Injected")
+                return True
+        if method != "GET":
+            self._send_json(writer, 405, _status(405, "MethodNotAllowed", method), "Method Not Allowed")
+            return True
+        if path == "/version":
+            self._send_json(writer, 200, {"major": "1", "minor": "33", "gitVersion": "v1.33.1-fake",
+                                          "platform": "linux/amd64"})
+            return True
+        if path == "/api/v1/namespaces":
+            names = sorted({ns for ns, _ in self.pods} | set(self.extra_namespaces))
+            items = [{"kind": "Namespace", "apiVersion": "v1",
+                      "metadata": {"name": n, "uid": str(uuid.uuid5(uuid.NAMESPACE_DNS, n))},
+                      "status": {"phase": "Active"}} for n in names]
+            self._send_json(writer, 200, self._paginate("NamespaceList", items, q))
+            return True
+        ns = None
+        if path.startswith("/api/v1/namespaces/") and path.endswith("/pods"):
+            ns = path[len("/api/v1/namespaces/"):-len("/pods")]
+        elif path != "/api/v1/pods":
+            self._send_json(writer, 404, _status(404, "NotFound", f"{path} not found"), "Not Found")
+            return True
+        if q.get("watch") in ("true", "1"):
+            await self._watch(writer, ns, q)
+            return False
+        pods = [p for (pns, _), p in sorted(self.pods.items())
+                if (ns is None or pns == ns) and _match_labels(p, q.get("labelSelector"))
+                and _match_fields(p, q.get("fieldSelector"))]
+        self._send_json(writer, 200, self._paginate("PodList", pods, q))
+        return True
+
+    def _paginate(self, kind: str, items: List[Dict[str, Any]], q: Dict[str, str]) -> Dict[str, Any]:
+        start = 0
+        rv = str(self.rv)
+        if q.get("continue"):
+            try:
+                tok = json.loads(base64.urlsafe_b64decode(q["continue"].encode()))
+                start, rv = int(tok["o"]), tok["rv"]
+            except (ValueError, KeyError):
+                start = 0
+        limit = int(q.get("limit") or 0)
+        end = len(items) if not limit else min(len(items), start + limit)
+        meta: Dict[str, Any] = {"resourceVersion": rv}
+        if end < len(items):
+            meta["continue"] = base64.urlsafe_b64encode(
+                json.dumps({"o": end, "rv": rv}).encode()).decode()
+            meta["remainingItemCount"] = len(items) - end
+        return {"kind": kind, "apiVersion": "v1", "metadata": meta, "items": items[start:end]}
+
+    async def _watch(self, writer, ns: Optional[str], q: Dict[str, str]) -> None:
+        w = _Watch(writer, ns, q.get("labelSelector"), q.get("fieldSelector"),
+                   q.get("allowWatchBookmarks") in ("true", "1"))
+        rv_param = q.get("resourceVersion")
+        if rv_param not in (None, "", "0"):
+            try:
+                since = int(rv_param)
+            except ValueError:
+                since = -1
+            if since < self.compacted_rv:
+                if self.expired_as_http_status:
+                    self._send_json(writer, 410, _status(410, "Expired", "too old resource version"), "Gone")
+                    await writer.drain()
+                    return
+                writer.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\n"
+                             b"Transfer-Encoding: chunked\r\n\r\n")
+                line = json.dumps({"type": "ERROR", "object": _status(
+                    410, "Expired", f"too old resource version: {since} ({self.compacted_rv})")}).encode()
+                writer.write(_chunk(line + b"\n") + b"0\r\n\r\n")
+                await writer.drain()
+                return
+            backlog = [line for (rv, _, pod, line) in self.history if rv > since and w.wants(pod)]
+        else:
+            backlog = [json.dumps({"type": "ADDED", "object": p}, separators=(",", ":"),
+                                  ensure_ascii=False).encode() + b"\n"
+                       for _, p in sorted(self.pods.items()) if w.wants(p)]
+        writer.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\n"
+                     b"Transfer-Encoding: chunked\r\n\r\n")
+        for line in backlog:
+            writer.write(_chunk(line))
+        self.watches.add(w)
+        timeout = q.get("timeoutSeconds")
+        try:
+            await writer.drain()
+            if timeout:
+                try:
+                    await with_timeout(w.closed.wait(), float(timeout))
+                except asyncio.TimeoutError:
+                    pass
+            else:
+                await w.closed.wait()
+        except ConnectionError:
+            pass
+        finally:
+            if w in self.watches:
+                self.watches.discard(w)
+                try:
+                    writer.write(b"0\r\n\r\n")
+                except Exception:  # noqa: BLE001
+                    pass
+
+
+class ServerThread:
+    """Run a :class:`FakeApiServer` on its own event loop in a daemon thread."""
+
+    def __init__(self, server: FakeApiServer, host: str = "127.0.0.1", port: int = 0) -> None:
+        self.server = server
+        self.loop = asyncio.new_event_loop()
+        self._ready = threading.Event()
+        self._host = host
+        self._port = port
+        self.thread = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self) -> None:
+        asyncio.set_event_loop(self.loop)
+        self.loop.run_until_complete(self.server.start(self._host, self._port))
+        self._ready.set()
+        self.loop.run_forever()
+
+    def start(self) -> "ServerThread":
+        self.thread.start()
+        self._ready.wait(10)
+        return self
+
+    def call(self, fn, *args, **kwargs):
+        """Run ``fn`` on the server loop and return its result."""
+        fut = asyncio.run_coroutine_threadsafe(self._wrap(fn, *args, **kwargs), self.loop)
+        return fut.result(10)
+
+    @staticmethod
+    async def _wrap(fn, *args, **kwargs):
+        res = fn(*args, **kwargs)
+        if asyncio.iscoroutine(res):
+            res = await res
+        return res
+
+    def stop(self) -> None:
+        try:
+            asyncio.run_coroutine_threadsafe(self.server.stop(), self.loop).result(5)
+        except Exception:  # noqa: BLE001
+            pass
+        self.loop.call_soon_threadsafe(self.loop.stop)
+        self.thread.join(5)
+
+
+def main(argv: Optional[List[str]] = None) -> None:
+    ap = argparse.ArgumentParser(description="fake kube-apiserver for k8s-watcher")
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=9988)
+    ap.add_argument("--token", default=None)
+    ap.add_argument("--pods", type=int, default=10, help="pods to pre-create")
+    ap.add_argument("--churn-rate", type=float, default=0.0, help="lifecycle events/s after start")
+    args = ap.parse_args(argv)
+
+    from .podgen import PodFactory, churn_events
+
+    async def run() -> None:
+        srv = FakeApiServer(token=args.token, bookmark_interval=30)
+        f = PodFactory(seed=1, namespaces=["default", "kube-system", "production", "monitoring"])
+        for _ in range(args.pods):
+            srv.create(f.running(f.new_pod()))
+        port = await srv.start(args.host, args.port)
+        print(f"fake kube-apiserver listening on http://{args.host}:{port}", flush=True)
+        if args.churn_rate > 0:
+            for et, obj in churn_events(10 ** 9, seed=2):
+                srv.apply(et, obj)
+                await asyncio.sleep(1.0 / args.churn_rate)
+        else:
+            await asyncio.Event().wait()
+
+    try:
+        asyncio.run(run())
+    except KeyboardInterrupt:
+        pass
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,229 @@
+"""Stub clusterapi sink (the receiving end of ``POST /api/pods/update``).
+
+The reference ships no clusterapi stub. This one:
+
+* answers ``POST <pod_update>`` (default ``/api/pods/update``) and
+  ``GET /health``; keep-alive and HTTP/1.1 pipelining are supported, with
+  responses kept in request order per connection;
+* records bodies (``record=True``) with their receive time so tests can
+  check schema, per-pod order and exactly-once delivery;
+* injects latency (fixed seconds) and failures (a status for a fraction of
+  requests, or for the next N requests);
+* is a raw ``asyncio.Protocol`` so that, in benchmarks, it is not the
+  bottleneck; :func:`run_sink_process` runs several SO_REUSEPORT workers.
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import collections
+import json
+import os
+import random
+import socket
+import time
+from typing import Deque, Dict, List, Optional, Tuple
+from ..utils.aio import with_timeout
+
+_OK = b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nContent-Length: 15\r\n\r\n{\"status\":\"ok\"}"
+
+
+def _resp(status: int, body: bytes = b"{}") -> bytes:
+    reason = {200: "OK", 201: "Created", 204: "No Content", 400: "Bad Request", 404: "Not Found",
+              429: "Too Many Requests", 500: "Internal Server Error",
+              503: "Service Unavailable"}.get(status, "Status")
+    if status == 204:
+        return b"HTTP/1.1 204 No Content\r\n\r\n"
+    return b"HTTP/1.1 %d %s\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n%s" % (
+        status, reason.encode(), len(body), body)
+
+
+class SinkState:
+    def __init__(self, path: str = "/api/pods/update", record: bool = True, latency: float = 0.0,
+                 fail_rate: float = 0.0, fail_status: int = 500, success_status: int = 200,
+                 seed: int = 0) -> None:
+        self.path = path.encode()
+        self.record = record
+        self.latency = latency
+        self.fail_rate = fail_rate
+        self.fail_status = fail_status
+        self.success_status = success_status
+        self.fail_next: List[int] = []
+        self.rng = random.Random(seed)
+        self.received: List[Tuple[int, bytes]] = []
+        self.count = 0
+        self.failed = 0
+        self.health_checks = 0
+        self.connections = 0
+        self.waiters: List[Tuple[int, asyncio.Future]] = []
+
+    def payloads(self) -> List[Dict]:
+        return [json.loads(b) for _, b in self.received]
+
+    def _notify_waiters(self) -> None:
+        if not self.waiters:
+            return
+        keep = []
+        for n, fut in self.waiters:
+            if self.count >= n and not fut.done():
+                fut.set_result(self.count)
+            elif not fut.done():
+                keep.append((n, fut))
+        self.waiters = keep
+
+    async def wait_for(self, n: int, timeout: float = 10.0) -> int:
+        if self.count >= n:
+            return self.count
+        fut = asyncio.get_running_loop().create_future()
+        self.waiters.append((n, fut))
+        return await with_timeout(fut, timeout)
+
+
+class _SinkProtocol(asyncio.Protocol):
+    def __init__(self, state: SinkState) -> None:
+        self.st = state
+        self.buf = bytearray()
+        self.transport: Optional[asyncio.Transport] = None
+        self.out: Deque[List] = collections.deque()  # [ready, bytes]
+
+    def connection_made(self, transport) -> None:  # type: ignore[override]
+        self.transport = transport
+        self.st.connections += 1
+
+    def data_received(self, data: bytes) -> None:  # type: ignore[override]
+        buf = self.buf
+        buf += data
+        st = self.st
+        pos = 0
+        responses: List[bytes] = []
+        now = time.monotonic_ns()
+        while True:
+            he = buf.find(b"\r\n\r\n", pos)
+            if he < 0:
+                break
+            head = bytes(buf[pos:he])
+            cl = 0
+            i = head.lower().find(b"content-length:")
+            if i >= 0:
+                j = head.find(b"\r\n", i)
+                cl = int(head[i + 15:j if j >= 0 else len(head)].strip())
+            if len(buf) - (he + 4) < cl:
+                break
+            body = bytes(buf[he + 4:he + 4 + cl])
+            pos = he + 4 + cl
+            sp1 = head.find(b" ")
+            sp2 = head.find(b" ", sp1 + 1)
+            method, path = head[:sp1], head[sp1 + 1:sp2]
+            if method == b"GET" and path.startswith(b"/health"):
+                st.health_checks += 1
+                responses.append(_resp(200, b'{"status":"healthy"}'))
+                continue
+            if method != b"POST" or path != st.path:
+                responses.append(_resp(404, b'{"error":"not found"}'))
+                continue
+            fail = None
+            if st.fail_next:
+                fail = st.fail_next.pop(0)
+            elif st.fail_rate and st.rng.random() < st.fail_rate:
+                fail = st.fail_status
+            if fail is not None:
+                st.failed += 1
+                responses.append(_resp(fail, b'{"error":"injected"}'))
+                continue
+            st.count += 1
+            if st.record:
+                st.received.append((now, body))
+            responses.append(_OK if st.success_status == 200 else _resp(st.success_status))
+        if pos:
+            del buf[:pos]
+        if responses:
+            st._notify_waiters()
+            payload = b"".join(responses)
+            if st.latency > 0:
+                item = [False, payload]
+                self.out.append(item)
+                asyncio.get_running_loop().call_later(st.latency, self._release, item)
+            else:
+                if self.out:
+                    self.out.append([True, payload])
+                    self._flush()
+                else:
+                    assert self.transport is not None
+                    self.transport.write(payload)
+
+    def _release(self, item: List) -> None:
+        item[0] = True
+        self._flush()
+
+    def _flush(self) -> None:
+        parts = []
+        while self.out and self.out[0][0]:
+            parts.append(self.out.popleft()[1])
+        if parts and self.transport is not None and not self.transport.is_closing():
+            self.transport.write(b"".join(parts))
+
+
+class StubSink:
+    def __init__(self, **kwargs) -> None:
+        self.state = SinkState(**kwargs)
+        self.server: Optional[asyncio.AbstractServer] = None
+        self.port = 0
+
+    async def start(self, host: str = "127.0.0.1", port: int = 0, reuse_port: bool = False,
+                    sock: Optional[socket.socket] = None) -> int:
+        loop = asyncio.get_running_loop()
+        if sock is not None:
+            self.server = await loop.create_server(lambda: _SinkProtocol(self.state), sock=sock)
+        else:
+            self.server = await loop.create_server(lambda: _SinkProtocol(self.state), host, port,
+                                                   reuse_port=reuse_port or None)
+        self.port = self.server.sockets[0].getsockname()[1]
+        return self.port
+
+    @property
+    def url(self) -> str:
+        return f"http://127.0.0.1:{self.port}"
+
+    async def stop(self) -> None:
+        if self.server is not None:
+            self.server.close()
+            try:
+                await with_timeout(self.server.wait_closed(), 2)
+            except asyncio.TimeoutError:
+                pass
+
+
+def run_sink_process(port: int, workers: int = 1, latency: float = 0.0) -> None:
+    """Blocking: serve on ``port`` with ``workers`` SO_REUSEPORT processes (bench helper)."""
+    pids = []
+    for _ in range(workers - 1):
+        pid = os.fork()
+        if pid == 0:
+            pids = []
+            break
+        pids.append(pid)
+
+    async def serve() -> None:
+        sink = StubSink(record=False, latency=latency)
+        await sink.start("127.0.0.1", port, reuse_port=True)
+        await asyncio.Event().wait()
+
+    try:
+        asyncio.run(serve())
+    except KeyboardInterrupt:
+        pass
+
+
+def main(argv: Optional[List[str]] = None) -> None:
+    ap = argparse.ArgumentParser(description="stub clusterapi sink")
+    ap.add_argument("--port", type=int, default=3000)
+    ap.add_argument("--workers", type=int, default=1)
+    ap.add_argument("--latency", type=float, default=0.0)
+    args = ap.parse_args(argv)
+    print(f"stub clusterapi listening on http://127.0.0.1:{args.port}", flush=True)
+    run_sink_process(args.port, args.workers, args.latency)
+
+
+if __name__ == "__main__":
+    main()

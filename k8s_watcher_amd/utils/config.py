@@ -1,0 +1,395 @@
+"""Layered YAML configuration.
+
+Reference behaviour being reproduced:
+
+* ``config/base.yaml`` then ``config/<env>.yaml`` are read with ``yaml.safe_load``;
+  an empty file counts as ``{}`` and a missing/broken file prints a message and
+  counts as ``{}`` (``/root/reference/watcher/pod_watcher.py:19-45``).
+* The environment file is deep-merged over the base: nested dicts merge
+  recursively, every other value (lists included) is replaced wholesale
+  (``pod_watcher.py:47-57``).
+* After the merge, any string that is *entirely* ``${VAR}`` or
+  ``${VAR:-default}`` is replaced by the environment variable (``""`` when
+  unset and no default). No inline interpolation, no type coercion
+  (``pod_watcher.py:59-75``).
+
+Deliberate differences (documented in docs/DEVIATIONS.md):
+
+* the config directory is CWD-relative like the reference, but can be
+  overridden (``K8S_WATCHER_CONFIG_DIR`` / ``--config-dir``) and falls back to
+  the directory that holds ``main.py`` when the CWD has no ``config/``;
+* the merge deep-copies, so callers can mutate the result safely;
+* :func:`settings_from_dict` turns the raw dict into a validated, typed
+  :class:`Settings` object; unknown keys are kept in ``Settings.raw``.
+"""
+
+from __future__ import annotations
+
+import copy
+import logging
+import os
+import sys
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+import yaml
+
+SUPPORTED_ENVIRONMENTS = ("development", "staging", "production")
+
+_REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+class ConfigError(ValueError):
+    """Raised for a configuration value that cannot be honoured."""
+
+
+# --------------------------------------------------------------------------- raw layer
+
+
+def resolve_config_dir(config_dir: Optional[str] = None) -> str:
+    """Pick the directory that holds ``base.yaml`` and the per-env files.
+
+    Precedence: explicit argument, ``$K8S_WATCHER_CONFIG_DIR``, ``./config``
+    (the reference's CWD-relative lookup, ``pod_watcher.py:22``), then the
+    ``config/`` directory next to this repository's ``main.py``.
+    """
+    if config_dir:
+        return config_dir
+    env_dir = os.environ.get("K8S_WATCHER_CONFIG_DIR")
+    if env_dir:
+        return env_dir
+    if os.path.isdir("config"):
+        return "config"
+    return os.path.join(_REPO_ROOT, "config")
+
+
+def load_config_file(path: str) -> Dict[str, Any]:
+    """Read one YAML file; ``{}`` for a missing, empty or unreadable file.
+
+    Messages are printed (not logged) because, as in the reference
+    (``pod_watcher.py:39-45``), logging is configured *from* this config.
+    """
+    try:
+        with open(path, "r", encoding="utf-8") as fh:
+            data = yaml.safe_load(fh)
+    except FileNotFoundError:
+        print(f"Config file {path} not found")
+        return {}
+    except Exception as exc:  # noqa: BLE001 - parity: any error -> {}
+        print(f"Error loading config {path}: {exc}")
+        return {}
+    if data is None:
+        return {}
+    if not isinstance(data, dict):
+        print(f"Error loading config {path}: top level must be a mapping, got {type(data).__name__}")
+        return {}
+    return data
+
+
+def deep_merge(base: Dict[str, Any], override: Dict[str, Any]) -> Dict[str, Any]:
+    """Recursive merge, override wins; lists/scalars are replaced, not joined."""
+    out = copy.deepcopy(base)
+    for key, value in override.items():
+        cur = out.get(key)
+        if isinstance(cur, dict) and isinstance(value, dict):
+            out[key] = deep_merge(cur, value)
+        else:
+            out[key] = copy.deepcopy(value)
+    return out
+
+
+def substitute_env(obj: Any, environ: Optional[Dict[str, str]] = None) -> Any:
+    """Replace whole-string ``${VAR}`` / ``${VAR:-default}`` values recursively."""
+    env = os.environ if environ is None else environ
+    if isinstance(obj, dict):
+        return {k: substitute_env(v, env) for k, v in obj.items()}
+    if isinstance(obj, list):
+        return [substitute_env(v, env) for v in obj]
+    if isinstance(obj, str) and obj.startswith("${") and obj.endswith("}"):
+        name = obj[2:-1]
+        default = ""
+        if ":-" in name:
+            name, default = name.split(":-", 1)
+        return env.get(name, default)
+    return obj
+
+
+def load_layered_config(environment: str, config_dir: Optional[str] = None,
+                        environ: Optional[Dict[str, str]] = None) -> Dict[str, Any]:
+    """base.yaml ⊕ <environment>.yaml, then env-var substitution."""
+    cdir = resolve_config_dir(config_dir)
+    base = load_config_file(os.path.join(cdir, "base.yaml"))
+    env_cfg = load_config_file(os.path.join(cdir, f"{environment}.yaml"))
+    return substitute_env(deep_merge(base, env_cfg), environ)
+
+
+def get_path(cfg: Dict[str, Any], dotted: str, default: Any = None) -> Any:
+    """``get_path(cfg, "watcher.alerts.critical_events_only")`` with a default."""
+    cur: Any = cfg
+    for part in dotted.split("."):
+        if not isinstance(cur, dict) or part not in cur:
+            return default
+        cur = cur[part]
+    return cur
+
+
+# --------------------------------------------------------------------------- typed layer
+
+
+def _as_bool(value: Any, key: str) -> bool:
+    if isinstance(value, bool):
+        return value
+    if value is None:
+        return False
+    if isinstance(value, (int, float)):
+        return bool(value)
+    if isinstance(value, str):
+        low = value.strip().lower()
+        if low in ("1", "true", "yes", "on"):
+            return True
+        if low in ("", "0", "false", "no", "off"):
+            return False
+    raise ConfigError(f"{key}: expected a boolean, got {value!r}")
+
+
+def _as_float(value: Any, key: str) -> float:
+    try:
+        return float(value)
+    except (TypeError, ValueError):
+        raise ConfigError(f"{key}: expected a number, got {value!r}") from None
+
+
+def _as_int(value: Any, key: str) -> int:
+    try:
+        out = int(value)
+    except (TypeError, ValueError):
+        raise ConfigError(f"{key}: expected an integer, got {value!r}") from None
+    return out
+
+
+def _choice(value: Any, key: str, choices: tuple) -> str:
+    if value not in choices:
+        raise ConfigError(f"{key}: expected one of {list(choices)}, got {value!r}")
+    return value
+
+
+@dataclass
+class RetryPolicy:
+    """Attempts/backoff for one retrying activity (``base.yaml`` ``retry:`` blocks).
+
+    The reference declares these blocks but never reads them;
+    here ``watcher.retry`` drives watch reconnects and ``clusterapi.retry``
+    drives notify retries.
+    """
+
+    max_attempts: int = 3
+    delay_seconds: float = 1.0
+    multiplier: float = 2.0
+    max_delay_seconds: float = 30.0
+    jitter: float = 0.1
+
+    def delay(self, attempt: int) -> float:
+        """Backoff before retry number ``attempt`` (1-based), without jitter."""
+        d = self.delay_seconds * (self.multiplier ** max(0, attempt - 1))
+        return min(d, self.max_delay_seconds)
+
+
+@dataclass
+class KubernetesSettings:
+    use_incluster_config: bool = False
+    config_file: Optional[str] = None
+    context: Optional[str] = None
+    use_mock: bool = False
+    request_timeout: float = 30.0
+
+
+@dataclass
+class NotifierPoolSettings:
+    connections: int = 16
+    pipeline_depth: int = 1
+    queue_size: int = 65536
+    coalesce: bool = False
+
+
+@dataclass
+class ClusterApiSettings:
+    enabled: bool = True
+    base_url: str = "http://localhost:3000"
+    api_key: str = ""
+    pod_update: str = "/api/pods/update"
+    health: str = "/health"
+    timeout: float = 30.0
+    retry: RetryPolicy = field(default_factory=lambda: RetryPolicy(3, 2.0))
+    pool: NotifierPoolSettings = field(default_factory=NotifierPoolSettings)
+    verify_tls: bool = True
+    ca_file: Optional[str] = None
+    health_check_on_start: bool = True
+
+
+@dataclass
+class CheckpointSettings:
+    path: Optional[str] = None
+    interval_seconds: float = 5.0
+
+
+@dataclass
+class MetricsSettings:
+    enabled: bool = False
+    host: str = "0.0.0.0"
+    port: int = 9090
+
+
+@dataclass
+class WatcherSettings:
+    log_level: str = "INFO"
+    log_file: Optional[str] = None
+    namespaces: List[str] = field(default_factory=list)
+    namespace_scope: str = "client"  # client | server
+    label_selector: Optional[str] = None
+    field_selector: Optional[str] = None
+    critical_events_only: bool = False
+    notify_on: str = "all"  # all | phase_change
+    initial_list: str = "notify"  # notify | skip
+    retry: RetryPolicy = field(default_factory=lambda: RetryPolicy(3, 5.0))
+    watch_timeout_seconds: int = 300
+    list_page_size: int = 500
+    watch_interval: float = 1.0  # accepted for schema parity; a watch has no poll interval
+    engine: str = "native"  # native | python
+    state_format: str = "structured"  # structured | python_repr
+    event_timestamp: str = "local"  # local | utc
+    log_events: Optional[bool] = None  # None = follow log level (parity)
+    checkpoint: CheckpointSettings = field(default_factory=CheckpointSettings)
+
+
+@dataclass
+class Settings:
+    environment: str
+    kubernetes: KubernetesSettings
+    watcher: WatcherSettings
+    clusterapi: ClusterApiSettings
+    metrics: MetricsSettings
+    raw: Dict[str, Any]
+
+    @property
+    def production(self) -> bool:
+        return self.environment == "production"
+
+
+def _retry(block: Any, key: str, default: RetryPolicy, min_attempts: int = 1) -> RetryPolicy:
+    if not isinstance(block, dict):
+        return copy.copy(default)
+    return RetryPolicy(
+        max_attempts=max(min_attempts, _as_int(block.get("max_attempts", default.max_attempts),
+                                               f"{key}.max_attempts")),
+        delay_seconds=max(0.0, _as_float(block.get("delay_seconds", default.delay_seconds), f"{key}.delay_seconds")),
+        multiplier=max(1.0, _as_float(block.get("backoff_multiplier", default.multiplier), f"{key}.backoff_multiplier")),
+        max_delay_seconds=_as_float(block.get("max_delay_seconds", default.max_delay_seconds), f"{key}.max_delay_seconds"),
+        jitter=_as_float(block.get("jitter", default.jitter), f"{key}.jitter"),
+    )
+
+
+def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
+    """Validate the merged dict into :class:`Settings` (raises :class:`ConfigError`)."""
+    k = cfg.get("kubernetes") or {}
+    w = cfg.get("watcher") or {}
+    c = cfg.get("clusterapi") or {}
+    m = cfg.get("metrics") or {}
+
+    kube = KubernetesSettings(
+        use_incluster_config=_as_bool(k.get("use_incluster_config", False), "kubernetes.use_incluster_config"),
+        config_file=k.get("config_file") or None,
+        context=k.get("context") or None,
+        use_mock=_as_bool(k.get("use_mock", False), "kubernetes.use_mock"),
+        request_timeout=_as_float(k.get("request_timeout", 30.0), "kubernetes.request_timeout"),
+    )
+
+    level = str(w.get("log_level", "INFO")).upper()
+    if not isinstance(logging.getLevelName(level), int):
+        raise ConfigError(f"watcher.log_level: unknown level {w.get('log_level')!r}")
+    namespaces = w.get("namespaces") or []
+    if not isinstance(namespaces, list) or not all(isinstance(n, str) for n in namespaces):
+        raise ConfigError(f"watcher.namespaces: expected a list of names, got {namespaces!r}")
+    alerts = w.get("alerts") or {}
+    ck = w.get("checkpoint") or {}
+    watcher = WatcherSettings(
+        log_level=level,
+        log_file=w.get("log_file") or None,
+        namespaces=list(namespaces),
+        namespace_scope=_choice(w.get("namespace_scope", "client"), "watcher.namespace_scope", ("client", "server")),
+        label_selector=w.get("label_selector") or None,
+        field_selector=w.get("field_selector") or None,
+        critical_events_only=_as_bool(alerts.get("critical_events_only", False), "watcher.alerts.critical_events_only"),
+        notify_on=_choice(w.get("notify_on", "all"), "watcher.notify_on", ("all", "phase_change")),
+        initial_list=_choice(w.get("initial_list", "notify"), "watcher.initial_list", ("notify", "skip")),
+        retry=_retry(w.get("retry"), "watcher.retry", RetryPolicy(3, 5.0), min_attempts=0),
+        watch_timeout_seconds=_as_int(w.get("watch_timeout_seconds", 300), "watcher.watch_timeout_seconds"),
+        list_page_size=max(1, _as_int(w.get("list_page_size", 500), "watcher.list_page_size")),
+        watch_interval=_as_float(w.get("watch_interval", 1), "watcher.watch_interval"),
+        engine=_choice(w.get("engine", "native"), "watcher.engine", ("native", "python")),
+        state_format=_choice(w.get("state_format", "structured"), "watcher.state_format", ("structured", "python_repr")),
+        event_timestamp=_choice(w.get("event_timestamp", "local"), "watcher.event_timestamp", ("local", "utc")),
+        log_events=None if w.get("log_events") is None else _as_bool(w.get("log_events"), "watcher.log_events"),
+        checkpoint=CheckpointSettings(
+            path=ck.get("path") or None,
+            interval_seconds=_as_float(ck.get("interval_seconds", 5.0), "watcher.checkpoint.interval_seconds"),
+        ),
+    )
+
+    endpoints = c.get("endpoints") or {}
+    auth = c.get("auth") or {}
+    pool = c.get("pool") or {}
+    clusterapi = ClusterApiSettings(
+        enabled=_as_bool(c.get("enabled", True), "clusterapi.enabled"),
+        base_url=str(c.get("base_url") or "http://localhost:3000").rstrip("/"),
+        api_key=str(auth.get("api_key") or ""),
+        pod_update=str(endpoints.get("pod_update", "/api/pods/update")),
+        health=str(endpoints.get("health", "/health")),
+        timeout=_as_float(c.get("timeout", 30), "clusterapi.timeout"),
+        retry=_retry(c.get("retry"), "clusterapi.retry", RetryPolicy(3, 2.0)),
+        pool=NotifierPoolSettings(
+            connections=max(1, _as_int(pool.get("connections", 16), "clusterapi.pool.connections")),
+            pipeline_depth=max(1, _as_int(pool.get("pipeline_depth", 1), "clusterapi.pool.pipeline_depth")),
+            queue_size=max(1, _as_int(pool.get("queue_size", 65536), "clusterapi.pool.queue_size")),
+            coalesce=_as_bool(pool.get("coalesce", False), "clusterapi.pool.coalesce"),
+        ),
+        verify_tls=_as_bool(c.get("verify_tls", True), "clusterapi.verify_tls"),
+        ca_file=c.get("ca_file") or None,
+        health_check_on_start=_as_bool(c.get("health_check_on_start", True), "clusterapi.health_check_on_start"),
+    )
+
+    metrics = MetricsSettings(
+        enabled=_as_bool(m.get("enabled", False), "metrics.enabled"),
+        host=str(m.get("host", "0.0.0.0")),
+        port=_as_int(m.get("port", 9090), "metrics.port"),
+    )
+    return Settings(environment, kube, watcher, clusterapi, metrics, cfg)
+
+
+def load_settings(environment: str, config_dir: Optional[str] = None,
+                  overrides: Optional[Dict[str, Any]] = None,
+                  environ: Optional[Dict[str, str]] = None) -> Settings:
+    """Full path: layered YAML → env substitution → optional overrides → :class:`Settings`."""
+    raw = load_layered_config(environment, config_dir, environ)
+    if overrides:
+        raw = deep_merge(raw, overrides)
+    return settings_from_dict(environment, raw)
+
+
+def parse_override(expr: str) -> Dict[str, Any]:
+    """``"watcher.notify_on=phase_change"`` → nested dict (value parsed as YAML)."""
+    if "=" not in expr:
+        raise ConfigError(f"override {expr!r}: expected key.path=value")
+    key, value = expr.split("=", 1)
+    node: Dict[str, Any] = {}
+    cur = node
+    parts = key.strip().split(".")
+    for part in parts[:-1]:
+        cur[part] = {}
+        cur = cur[part]
+    cur[parts[-1]] = yaml.safe_load(value)
+    return node
+
+
+def dump_effective(settings: Settings, stream=None) -> None:
+    """Print the merged raw config as YAML (``--print-config``)."""
+    yaml.safe_dump(settings.raw, stream or sys.stdout, sort_keys=False)
