@@ -1,0 +1,319 @@
+#!/usr/bin/env python3
+"""Headline benchmark: sustained pod-events/s + p50 event→notify latency.
+
+BASELINE.json metric: "pod-events/sec sustained + p50 event→notify latency
+(single process, mock API)"; its throughput config is #4: ``production.yaml``,
+all-namespaces watch, 10k-pod churn, async HTTP notifier pool. The reference
+publishes no numbers, so the reference-equivalent pipeline
+(``benchmarks/reference_equiv.py``) is measured on the same replay in the same
+run and ``vs_baseline`` is the ratio to it.
+
+Per rank (one watcher process per rank; ``torchrun`` ranks = independent
+namespace shards, weak scaling):
+
+* a replay API server child (``testing/replay_server.py``) streams one *step* =
+  ``--pods-per-step`` pod lifecycles (ADDED → 3×MODIFIED → DELETED, ≈4 KB of
+  real-shaped Pod JSON per event, one HTTP chunk per event);
+* a stub clusterapi child (``testing/stub_sink.py``) acks every POST;
+* this process runs the real :class:`WatcherService` (production profile:
+  critical-events filter, namespace filter, notifier pool) and a step ends when
+  every event of the step has been decoded, filtered and — if it survived the
+  filters — POSTed and acknowledged (2xx) by the sink.
+
+``W`` warmup steps run untimed, then exactly ``K`` steps are timed between
+barriers; the slowest rank's time is used. Latency (socket read of the watch
+chunk → 2xx from clusterapi) is measured afterwards at the config's nominal
+rate (``--latency-rate``, default 100 ev/s as in config #4).
+
+Usage: ``python bench.py [--gpus N] [--steps K] [--warmup W]`` (one JSON line on
+rank 0). There is no device work in this workload — see SURVEY.md §2.2 — so
+there is nothing to ``torch.cuda.synchronize()``; the barrier (gloo, for N>1)
+brackets the timed region.
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import signal
+import socket
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "pod-events/sec sustained + p50 event→notify latency (single process, mock API)"
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one watcher process each)")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pods-per-step", type=int, default=10000, help="pod lifecycles per step (5 events each)")
+    ap.add_argument("--profile", default="production", choices=["development", "staging", "production"])
+    ap.add_argument("--engine", default="native", choices=["native", "python"])
+    ap.add_argument("--connections", type=int, default=None, help="notifier pool connections")
+    ap.add_argument("--pipeline-depth", type=int, default=None)
+    ap.add_argument("--sink-workers", type=int, default=2)
+    ap.add_argument("--latency-rate", type=float, default=100.0)
+    ap.add_argument("--latency-seconds", type=float, default=3.0)
+    ap.add_argument("--ref-events", type=int, default=10000,
+                    help="events for the reference-equivalent run (0 = skip, vs_baseline null)")
+    ap.add_argument("--step-timeout", type=float, default=300.0)
+    ap.add_argument("--json-out", default=None, help="also write the result line to this file")
+    return ap.parse_args(argv)
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class Dist:
+    """gloo process group when launched by torchrun with WORLD_SIZE > 1."""
+
+    def __init__(self) -> None:
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
+
+    def barrier(self) -> None:
+        if self.world > 1:
+            self.dist.barrier()
+
+    def reduce(self, value: float, op: str) -> float:
+        if self.world == 1:
+            return value
+        import torch
+        t = torch.tensor([value], dtype=torch.float64)
+        self.dist.all_reduce(t, op=getattr(self.dist.ReduceOp, op))
+        return float(t.item())
+
+    def close(self) -> None:
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+async def spawn(*cmd: str):
+    return await asyncio.create_subprocess_exec(
+        *cmd, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
+        stderr=asyncio.subprocess.DEVNULL, start_new_session=True, cwd=ROOT)
+
+
+async def rank_main(args, d: Dist) -> dict:
+    from k8s_watcher_amd.engine.service import WatcherService
+    from k8s_watcher_amd.kube.kubeconfig import KubeEndpoint
+    from k8s_watcher_amd.metrics import Metrics
+    from k8s_watcher_amd.utils.config import load_settings
+    from k8s_watcher_amd.utils.logsetup import setup_logging
+
+    replay = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.replay_server",
+                         "--pods-per-step", str(args.pods_per_step), "--seed", str(d.rank))
+    sink_port = free_port()
+    sink = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.stub_sink", "--port", str(sink_port),
+                       "--workers", str(args.sink_workers))
+    try:
+        ready = (await asyncio.wait_for(replay.stdout.readline(), 600)).decode().split()
+        assert ready and ready[0] == "READY", ready
+        api_port, events_per_step = int(ready[1]), int(ready[2])
+        await asyncio.wait_for(sink.stdout.readline(), 60)
+        await asyncio.sleep(0.3)  # let every SO_REUSEPORT worker bind
+
+        async def cmd(line: str) -> int:
+            replay.stdin.write((line + "\n").encode())
+            await replay.stdin.drain()
+            reply = (await replay.stdout.readline()).decode().split()
+            return int(reply[2])
+
+        log_path = os.path.join("/tmp", f"k8s-watcher-bench-{os.getpid()}.log")
+        setup_logging(args.profile, "WARNING" if args.profile == "production" else "INFO", log_file=log_path)
+        overrides = {
+            "clusterapi": {"base_url": f"http://127.0.0.1:{sink_port}", "timeout": 30},
+            "watcher": {"engine": args.engine, "retry": {"max_attempts": 0, "delay_seconds": 0.05}},
+        }
+        pool = {}
+        if args.connections:
+            pool["connections"] = args.connections
+        if args.pipeline_depth:
+            pool["pipeline_depth"] = args.pipeline_depth
+        if pool:
+            overrides["clusterapi"]["pool"] = pool
+        settings = load_settings(args.profile, overrides=overrides)
+        if settings.watcher.log_level:
+            setup_logging(args.profile, settings.watcher.log_level, log_file=log_path)
+        metrics = Metrics(record_samples=True)
+        svc = WatcherService(settings, endpoint=KubeEndpoint(server=f"http://127.0.0.1:{api_port}"),
+                             metrics=metrics)
+        await svc.start()
+        for _ in range(200):
+            if await cmd("WATCHERS 0") >= 1:
+                break
+            await asyncio.sleep(0.01)
+
+        c = metrics.c
+
+        async def run_step(k: int, pace: str = "") -> None:
+            base = c["events_received"]
+            n = await cmd(f"PACE {k} {pace}" if pace else f"STEP {k}")
+            deadline = time.monotonic() + args.step_timeout
+            while c["events_received"] < base + n or svc.notifier.outstanding() > 0:
+                if time.monotonic() > deadline:
+                    raise TimeoutError(f"step {k}: {c['events_received'] - base}/{n} events, "
+                                       f"{svc.notifier.outstanding()} notifications outstanding")
+                await asyncio.sleep(0.0005)
+
+        for k in range(args.warmup):
+            await run_step(k)
+        metrics.latency.reset()
+        d.barrier()
+        n0, s0 = c["events_received"], c["notify_delivered"]
+        t0 = time.perf_counter()
+        for k in range(args.warmup, args.warmup + args.steps):
+            await run_step(k)
+        elapsed = time.perf_counter() - t0
+        d.barrier()
+        events = c["events_received"] - n0
+        notified = c["notify_delivered"] - s0
+        sat_p50 = metrics.latency.percentile_ns(50)
+
+        # latency at the nominal rate (untimed)
+        metrics.latency.reset()
+        count = max(1, int(args.latency_rate * args.latency_seconds))
+        await run_step(args.warmup + args.steps, f"{args.latency_rate} {count}")
+        p50 = metrics.latency.percentile_ns(50)
+        p99 = metrics.latency.percentile_ns(99)
+        lat_n = metrics.latency.n
+        failed = c["notify_failed"]
+        svc.stop()
+        await svc.shutdown()
+
+        ref = None
+        if args.ref_events > 0 and d.rank == 0:
+            ref = await run_reference(args, api_port, sink_port, cmd, args.warmup + args.steps + 1)
+        replay.stdin.write(b"QUIT\n")
+        await replay.stdin.drain()
+        return {"elapsed": elapsed, "events": events, "notified": notified, "events_per_step": events_per_step,
+                "p50_ns": p50, "p99_ns": p99, "lat_samples": lat_n, "sat_p50_ns": sat_p50,
+                "failed": failed, "ref": ref}
+    finally:
+        for p in (replay, sink):
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except (ProcessLookupError, PermissionError):
+                pass
+            try:
+                await asyncio.wait_for(p.wait(), 5)
+            except asyncio.TimeoutError:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+
+
+async def run_reference(args, api_port: int, sink_port: int, cmd, step: int) -> dict:
+    from benchmarks.reference_equiv import RefEquivWatcher
+    from k8s_watcher_amd.utils.config import load_settings
+
+    s = load_settings(args.profile)
+    ref = RefEquivWatcher(args.profile, s.watcher.namespaces, s.watcher.critical_events_only,
+                          f"http://127.0.0.1:{sink_port}")
+    loop = asyncio.get_running_loop()
+    connected = loop.create_future()
+    result = {}
+
+    def work() -> None:
+        result["elapsed"] = ref.run(f"http://127.0.0.1:{api_port}", args.ref_events,
+                                    on_connected=lambda: loop.call_soon_threadsafe(connected.set_result, None))
+
+    for _ in range(500):
+        if await cmd("WATCHERS 0") == 0:
+            break
+        await asyncio.sleep(0.01)
+    th = threading.Thread(target=work, daemon=True)
+    th.start()
+    await connected
+    for _ in range(200):
+        if await cmd("WATCHERS 0") >= 1:
+            break
+        await asyncio.sleep(0.01)
+    await cmd(f"PACE {step} 0 {args.ref_events}")
+    while th.is_alive():
+        await asyncio.sleep(0.01)
+    lat = sorted(ref.latencies_ns)
+    p50 = lat[len(lat) // 2] if lat else None
+    return {"events": ref.processed, "elapsed": result.get("elapsed"), "notified": ref.notified,
+            "events_per_s": ref.processed / result["elapsed"] if result.get("elapsed") else None,
+            "sat_p50_ns": p50}
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    d = Dist()
+    res = asyncio.run(rank_main(args, d))
+    elapsed = d.reduce(res["elapsed"], "MAX")
+    events = d.reduce(float(res["events"]), "SUM")
+    notified = d.reduce(float(res["notified"]), "SUM")
+    p50 = d.reduce(res["p50_ns"] or 0.0, "MAX")
+    p99 = d.reduce(res["p99_ns"] or 0.0, "MAX")
+    d.close()
+    if d.rank != 0:
+        return 0
+    value = events / elapsed
+    ref = res["ref"]
+    ref_rate = ref["events_per_s"] if ref else None
+    per_rank = value / d.world
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "pod-events/s",
+        "n_gpus": d.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1000, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(per_rank / ref_rate, 2) if ref_rate else None,
+        "dtype": "n/a",
+        "data": "synthetic",
+        "config": {
+            "model": f"k8s-watcher {args.profile} profile (BASELINE config #4: all-namespaces watch, "
+                     f"{args.pods_per_step}-pod churn, async notifier pool)",
+            "global_batch": int(res["events_per_step"] * d.world),
+            "seq_len": None,
+            "parallelism": f"shard{d.world}" if d.world > 1 else "single-process",
+            "engine": args.engine,
+        },
+        "p50_latency_ms": round(p50 / 1e6, 3) if p50 else None,
+        "p99_latency_ms": round(p99 / 1e6, 3) if p99 else None,
+        "latency_rate_ev_s": args.latency_rate,
+        "latency_samples": res["lat_samples"],
+        "notified_per_s": round(notified / elapsed, 1),
+        "notify_failed": res["failed"],
+        "saturated_p50_latency_ms": round(res["sat_p50_ns"] / 1e6, 3) if res["sat_p50_ns"] else None,
+        "reference_equiv": ({"events_per_s": round(ref_rate, 1), "events": ref["events"],
+                             "notified": ref["notified"],
+                             "saturated_p50_latency_ms": round(ref["sat_p50_ns"] / 1e6, 3)
+                             if ref["sat_p50_ns"] else None} if ref else None),
+        "baseline_source": "reference-equivalent pipeline measured in this run on the same replay "
+                           "(BASELINE.md: reference publishes no numbers)",
+    }
+    line = json.dumps(out)
+    print(line, flush=True)
+    if args.json_out:
+        with open(args.json_out, "w") as fh:
+            fh.write(line + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

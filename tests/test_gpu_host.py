@@ -1,0 +1,42 @@
+"""Host-tier tests run on the MI355X box (``-m gpu``).
+
+The watcher has no device work; what must hold on the
+deployment host is that the in-tree native decoder is the code that runs, the
+end-to-end path works there, and the headline bench produces a valid line.
+"""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def test_native_extension_loaded_in_tree():
+    from k8s_watcher_amd.ops import native
+    mod = native.load()
+    assert os.path.realpath(mod.__file__).startswith(os.path.realpath(ROOT))
+    assert mod.cpu_features()["avx2"] in (True, False)
+
+
+def test_smoke_end_to_end():
+    sys.path.insert(0, ROOT)
+    import __graft_entry__
+    __graft_entry__.smoke()
+
+
+def test_bench_line_is_valid():
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                          "--pods-per-step", "1000", "--ref-events", "500", "--latency-seconds", "1"],
+                         capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "vs_baseline"):
+        assert key in line
+    assert line["value"] > 0 and line["n_gpus"] == 1 and line["steps"] == 2
+    assert line["notify_failed"] == 0
