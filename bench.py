@@ -59,7 +59,7 @@ def parse_args(argv=None):
     ap.add_argument("--engine", default="native", choices=["native", "python"])
     ap.add_argument("--connections", type=int, default=None, help="notifier pool connections")
     ap.add_argument("--pipeline-depth", type=int, default=None)
-    ap.add_argument("--sink-workers", type=int, default=2)
+    ap.add_argument("--sink-workers", type=int, default=4)
     ap.add_argument("--latency-rate", type=float, default=100.0)
     ap.add_argument("--latency-seconds", type=float, default=3.0)
     ap.add_argument("--ref-events", type=int, default=10000,
@@ -118,7 +118,8 @@ async def rank_main(args, d: Dist) -> dict:
     from k8s_watcher_amd.utils.logsetup import setup_logging
 
     replay = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.replay_server",
-                         "--pods-per-step", str(args.pods_per_step), "--seed", str(d.rank))
+                         "--pods-per-step", str(args.pods_per_step), "--seed", str(d.rank),
+                         "--prerender", str(args.warmup + args.steps))
     sink_port = free_port()
     sink = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.stub_sink", "--port", str(sink_port),
                        "--workers", str(args.sink_workers))
@@ -138,7 +139,8 @@ async def rank_main(args, d: Dist) -> dict:
         log_path = os.path.join("/tmp", f"k8s-watcher-bench-{os.getpid()}.log")
         setup_logging(args.profile, "WARNING" if args.profile == "production" else "INFO", log_file=log_path)
         overrides = {
-            "clusterapi": {"base_url": f"http://127.0.0.1:{sink_port}", "timeout": 30},
+            "clusterapi": {"base_url": f"http://127.0.0.1:{sink_port}", "timeout": 30,
+                           "enabled": not os.environ.get("BENCH_NO_NOTIFY")},
             "watcher": {"engine": args.engine, "retry": {"max_attempts": 0, "delay_seconds": 0.05}},
         }
         pool = {}
@@ -162,15 +164,26 @@ async def rank_main(args, d: Dist) -> dict:
 
         c = metrics.c
 
+        debug = bool(os.environ.get("BENCH_DEBUG"))
+
         async def run_step(k: int, pace: str = "") -> None:
             base = c["events_received"]
+            t_start = time.perf_counter()
             n = await cmd(f"PACE {k} {pace}" if pace else f"STEP {k}")
+            t_sent = time.perf_counter()
+            t_ingest = None
             deadline = time.monotonic() + args.step_timeout
             while c["events_received"] < base + n or svc.notifier.outstanding() > 0:
+                if t_ingest is None and c["events_received"] >= base + n:
+                    t_ingest = time.perf_counter()
                 if time.monotonic() > deadline:
                     raise TimeoutError(f"step {k}: {c['events_received'] - base}/{n} events, "
                                        f"{svc.notifier.outstanding()} notifications outstanding")
                 await asyncio.sleep(0.0005)
+            if debug:
+                t_end = time.perf_counter()
+                print(f"step {k}: sent {t_sent - t_start:.3f}s ingest "
+                      f"{(t_ingest or t_end) - t_start:.3f}s done {t_end - t_start:.3f}s", file=sys.stderr)
 
         for k in range(args.warmup):
             await run_step(k)
@@ -218,6 +231,9 @@ async def rank_main(args, d: Dist) -> dict:
                     os.killpg(p.pid, signal.SIGKILL)
                 except (ProcessLookupError, PermissionError):
                     pass
+            transport = getattr(p, "_transport", None)
+            if transport is not None:
+                transport.close()  # close pipes while the loop is alive (no __del__ noise)
 
 
 async def run_reference(args, api_port: int, sink_port: int, cmd, step: int) -> dict:

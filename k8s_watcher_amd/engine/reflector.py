@@ -139,9 +139,18 @@ class Reflector:
         self._error = False
         pipeline = self.pipeline
         decoder = self.decoder
+        framed = [False]
+
+        def on_mode(is_framed: bool) -> None:
+            framed[0] = is_framed
 
         def sink(data: bytes, read_ns: int) -> None:
-            evs = decoder.feed(data)
+            if framed[0]:
+                evs = decoder.feed_chunked(data)
+                if decoder.body_done() and self.stream is not None:
+                    self.stream.close()  # server ended the watch (timeoutSeconds)
+            else:
+                evs = decoder.feed(data)
             if evs:
                 ctrl = pipeline.handle_batch(evs, read_ns)
                 if pipeline.last_rv:
@@ -153,7 +162,8 @@ class Reflector:
         self.stream = await self.api.watch_pods(
             sink, namespace=self.namespace, resource_version=self.rv,
             timeout_seconds=w.watch_timeout_seconds or None, allow_bookmarks=True,
-            label_selector=w.label_selector, field_selector=w.field_selector)
+            label_selector=w.label_selector, field_selector=w.field_selector,
+            raw_chunked=True, on_mode=on_mode)
         self.watch_count += 1
         self.connected.set()
         if self._stop.is_set():

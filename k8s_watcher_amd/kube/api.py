@@ -89,8 +89,13 @@ class KubeApi:
                          resource_version: Optional[str] = None, timeout_seconds: Optional[int] = None,
                          allow_bookmarks: bool = True, label_selector: Optional[str] = None,
                          field_selector: Optional[str] = None,
-                         connect_timeout: Optional[float] = None) -> StreamResponse:
-        """Open ``?watch=true``; de-chunked body bytes go to ``sink(data, read_ns)``."""
+                         connect_timeout: Optional[float] = None, raw_chunked: bool = False,
+                         on_mode: Optional[Callable[[bool], None]] = None) -> StreamResponse:
+        """Open ``?watch=true``; body bytes go to ``sink(data, read_ns)``.
+
+        With ``raw_chunked`` the HTTP chunk framing is left in place for the
+        decoder to strip natively; ``on_mode(framed)`` reports which it got.
+        """
         q: Dict[str, object] = {"watch": "true"}
         if resource_version:
             q["resourceVersion"] = resource_version
@@ -103,7 +108,8 @@ class KubeApi:
         if field_selector:
             q["fieldSelector"] = field_selector
         stream, err = await self.http.stream("GET", pods_path(namespace), sink, query=q,
-                                             timeout=connect_timeout)
+                                             timeout=connect_timeout, raw_chunked=raw_chunked,
+                                             on_mode=on_mode)
         if err is not None:
             raise ApiError(stream.status, stream.reason, err)
         return stream

@@ -68,12 +68,12 @@ class ResponseParser:
     responses to HEAD requests.
     """
 
-    HEAD, LENGTH, CHUNK_SIZE, CHUNK_DATA, CHUNK_CRLF, TRAILER, UNTIL_CLOSE, DONE = range(8)
+    HEAD, LENGTH, CHUNK_SIZE, CHUNK_DATA, CHUNK_CRLF, TRAILER, UNTIL_CLOSE, DONE, RAW = range(9)
 
     def __init__(self) -> None:
         self.reset()
 
-    def reset(self, no_body: bool = False) -> None:
+    def reset(self, no_body: bool = False, raw_chunked: bool = False) -> None:
         self.state = self.HEAD
         self.buf = bytearray()
         self.status = 0
@@ -83,23 +83,32 @@ class ResponseParser:
         self.body_parts: List[bytes] = []
         self.keep_alive = True
         self.no_body = no_body
+        # raw_chunked: hand a 2xx chunked body to on_body *with* its chunk framing
+        # (RAW state); the consumer de-chunks natively (``_kwcore``) and owns EOF.
+        self.raw_chunked = raw_chunked
+        self.chunked = False
         self.on_head: Optional[Callable[["ResponseParser"], None]] = None
         self.on_body: Optional[Callable[[bytes], None]] = None
         self.on_complete: Optional[Callable[["ResponseParser"], None]] = None
 
     # ------------------------------------------------------------------ helpers
     def _emit(self, data: bytes) -> None:
-        if not data:
-            return
-        if self.on_body is not None:
-            self.on_body(data)
-        else:
+        if data:
             self.body_parts.append(data)
+
+    def _flush_body(self) -> None:
+        # One callback per feed(): all chunks that arrived in one socket read
+        # reach the consumer together (the watch decoder batches on this).
+        if self.on_body is not None and self.body_parts:
+            parts = self.body_parts
+            self.body_parts = []
+            self.on_body(parts[0] if len(parts) == 1 else b"".join(parts))
 
     def body(self) -> bytes:
         return b"".join(self.body_parts)
 
     def _finish(self) -> None:
+        self._flush_body()
         self.state = self.DONE
         if self.on_complete is not None:
             self.on_complete(self)
@@ -133,7 +142,8 @@ class ResponseParser:
         if self.no_body or self.status in (204, 304) or 100 <= self.status < 200:
             self.state = self.DONE
         elif "chunked" in hdrs.get("transfer-encoding", "").lower():
-            self.state = self.CHUNK_SIZE
+            self.chunked = True
+            self.state = self.RAW if (self.raw_chunked and 200 <= self.status < 300) else self.CHUNK_SIZE
         elif "content-length" in hdrs:
             self.remaining = int(hdrs["content-length"])
             self.state = self.LENGTH if self.remaining > 0 else self.DONE
@@ -144,6 +154,12 @@ class ResponseParser:
     # ------------------------------------------------------------------ feeding
     def feed(self, data: bytes) -> bytes:
         """Consume ``data``; returns bytes left over after a complete message."""
+        if self.state == self.RAW and not self.buf:
+            if self.on_body is not None:  # hot path: framed watch bytes straight through
+                self.on_body(data)
+            else:
+                self.body_parts.append(data)
+            return b""
         buf = self.buf
         buf += data
         pos = 0
@@ -209,13 +225,14 @@ class ResponseParser:
                 if empty:
                     self._finish()
                     break
-            elif st == self.UNTIL_CLOSE:
+            elif st == self.UNTIL_CLOSE or st == self.RAW:
                 if pos < n:
                     self._emit(bytes(buf[pos:]))
                     pos = n
                 break
             else:  # DONE
                 break
+        self._flush_body()
         rest = b""
         if self.state == self.DONE:
             rest = bytes(buf[pos:])
@@ -225,7 +242,7 @@ class ResponseParser:
         return rest
 
     def feed_eof(self) -> None:
-        if self.state == self.UNTIL_CLOSE:
+        if self.state in (self.UNTIL_CLOSE, self.RAW):
             self._finish()
         elif self.state != self.DONE:
             raise HttpError("connection closed mid-response")
@@ -244,18 +261,23 @@ class _ClientProtocol(asyncio.Protocol):
         self.stream_sink: Optional[Callable[[bytes, int], None]] = None
         self.stream_head: Optional[asyncio.Future] = None
         self.last_activity = time.monotonic()
+        self.read_stamp = 0
+
+    def deliver(self, data: bytes) -> None:
+        """``parser.on_body`` for streams: body bytes + the socket-read timestamp."""
+        sink = self.stream_sink
+        if sink is not None:
+            sink(data, self.read_stamp)
 
     # asyncio callbacks
     def connection_made(self, transport) -> None:  # type: ignore[override]
         self.transport = transport
 
     def data_received(self, data: bytes) -> None:  # type: ignore[override]
-        self.last_activity = time.monotonic()
+        now = time.monotonic_ns()
+        self.read_stamp = now
+        self.last_activity = now * 1e-9
         try:
-            if self.stream_sink is not None:
-                stamp = time.monotonic_ns()
-                sink = self.stream_sink
-                self.parser.on_body = lambda b: sink(b, stamp)
             self.parser.feed(data)
         except Exception as exc:  # noqa: BLE001
             self._fail(exc)
@@ -445,8 +467,14 @@ class HttpClient:
     async def stream(self, method: str, path: str, sink: Callable[[bytes, int], None],
                      query: Optional[Dict[str, object]] = None,
                      headers: Optional[Dict[str, str]] = None,
-                     timeout: Optional[float] = None) -> Tuple[StreamResponse, Optional[bytes]]:
+                     timeout: Optional[float] = None, raw_chunked: bool = False,
+                     on_mode: Optional[Callable[[bool], None]] = None
+                     ) -> Tuple[StreamResponse, Optional[bytes]]:
         """Start a request whose body is streamed to ``sink(data, read_ns)``.
+
+        With ``raw_chunked`` a 2xx chunked body is passed through *with* its
+        chunk framing; ``on_mode(framed)`` is called once, before any body
+        byte, to tell the consumer which form it will receive.
 
         Returns ``(stream, error_body)``: for a non-2xx status the whole body
         is read and returned as ``error_body`` and the connection is closed.
@@ -460,7 +488,7 @@ class HttpClient:
         head_fut = loop.create_future()
         proto.stream_head = head_fut
         parser = proto.parser
-        parser.reset()
+        parser.reset(raw_chunked=raw_chunked)
         err_parts: List[bytes] = []
 
         def _on_head(p: ResponseParser) -> None:
@@ -469,6 +497,9 @@ class HttpClient:
                 p.on_body = err_parts.append
                 p.on_complete = lambda _p: (not head_fut.done()) and head_fut.set_result(False)
                 return
+            if on_mode is not None:
+                on_mode(p.state == ResponseParser.RAW)
+            p.on_body = proto.deliver
             if not head_fut.done():
                 head_fut.set_result(True)
 

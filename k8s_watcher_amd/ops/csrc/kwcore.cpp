@@ -732,9 +732,14 @@ struct DecoderObject {
     std::string* out;
     PodSpans* spans;
     InternTable* interned;
+    std::string* chunk_line;  // partial chunk-size / trailer line
+    int cstate;               // chunked-framing state (CS_*)
+    size_t cremain;           // bytes left in the current chunk
     long long n_events;
     long long n_bytes;
 };
+
+int hexval(char c);
 
 PyObject* make_invalid(const char* why, const char* line, size_t n) {
     PyObject* msg = PyUnicode_FromFormat("%s: %.200s", why, std::string(line, n < 200 ? n : 200).c_str());
@@ -905,6 +910,9 @@ PyObject* Decoder_new(PyTypeObject* type, PyObject*, PyObject*) {
     self->out->reserve(8192);
     self->spans = new PodSpans();
     self->interned = new InternTable();
+    self->chunk_line = new std::string();
+    self->cstate = 0;
+    self->cremain = 0;
     self->n_events = 0;
     self->n_bytes = 0;
     return (PyObject*)self;
@@ -916,6 +924,7 @@ void Decoder_dealloc(DecoderObject* self) {
     delete self->out;
     delete self->spans;
     delete self->interned;
+    delete self->chunk_line;
     Py_TYPE(self)->tp_free((PyObject*)self);
 }
 
@@ -925,20 +934,11 @@ bool blank(const char* b, size_t n) {
     return true;
 }
 
-PyObject* Decoder_feed(DecoderObject* self, PyObject* arg) {
-    Py_buffer view;
-    if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) < 0) return nullptr;
-    const char* data = (const char*)view.buf;
-    size_t n = (size_t)view.len;
-    self->n_bytes += (long long)n;
-    PyObject* out = PyList_New(0);
-    if (!out) {
-        PyBuffer_Release(&view);
-        return nullptr;
-    }
+// Split `data` into NDJSON lines (carrying a partial line across calls) and
+// append one event tuple per complete non-blank line to `out`.
+bool process_segment(DecoderObject* self, const char* data, size_t n, PyObject* out) {
     std::string& partial = *self->partial;
     size_t pos = 0;
-    bool ok = true;
     auto emit = [&](const char* b, size_t len) -> bool {
         if (len == 0 || blank(b, len)) return true;
         PyObject* t = decode_line(self, b, len);
@@ -951,22 +951,138 @@ PyObject* Decoder_feed(DecoderObject* self, PyObject* arg) {
         const char* nl = (const char*)std::memchr(data, '\n', n);
         if (!nl) {
             partial.append(data, n);
-            PyBuffer_Release(&view);
-            return out;
+            return true;
         }
         partial.append(data, (size_t)(nl - data));
-        ok = emit(partial.data(), partial.size());
+        bool ok = emit(partial.data(), partial.size());
         partial.clear();
+        if (!ok) return false;
         pos = (size_t)(nl - data) + 1;
     }
-    while (ok && pos < n) {
+    while (pos < n) {
         const char* nl = (const char*)std::memchr(data + pos, '\n', n - pos);
         if (!nl) {
             partial.assign(data + pos, n - pos);
             break;
         }
-        ok = emit(data + pos, (size_t)(nl - (data + pos)));
+        if (!emit(data + pos, (size_t)(nl - (data + pos)))) return false;
         pos = (size_t)(nl - data) + 1;
+    }
+    return true;
+}
+
+PyObject* Decoder_feed(DecoderObject* self, PyObject* arg) {
+    Py_buffer view;
+    if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) < 0) return nullptr;
+    self->n_bytes += (long long)view.len;
+    PyObject* out = PyList_New(0);
+    if (out && !process_segment(self, (const char*)view.buf, (size_t)view.len, out)) {
+        Py_DECREF(out);
+        out = nullptr;
+    }
+    PyBuffer_Release(&view);
+    return out;
+}
+
+// HTTP/1.1 chunked transfer framing, decoded in place of the Python parser
+// for the watch stream: size line → data → CRLF ... → 0-size chunk → trailers.
+enum { CS_SIZE, CS_DATA, CS_DATA_END, CS_TRAILER, CS_DONE };
+
+bool parse_chunk_size(const std::string& line, size_t& size) {
+    size_t v = 0;
+    size_t i = 0, n = line.size();
+    while (i < n && (line[i] == ' ' || line[i] == '\t')) ++i;
+    size_t start = i;
+    for (; i < n; ++i) {
+        int h = hexval(line[i]);
+        if (h < 0) break;
+        if (v > (SIZE_MAX >> 4)) return false;
+        v = (v << 4) | (size_t)h;
+    }
+    if (i == start) return false;
+    while (i < n && (line[i] == ' ' || line[i] == '\t' || line[i] == '\r')) ++i;
+    if (i < n && line[i] != ';') return false;
+    size = v;
+    return true;
+}
+
+PyObject* Decoder_feed_chunked(DecoderObject* self, PyObject* arg) {
+    Py_buffer view;
+    if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) < 0) return nullptr;
+    const char* data = (const char*)view.buf;
+    size_t n = (size_t)view.len;
+    self->n_bytes += (long long)n;
+    PyObject* out = PyList_New(0);
+    if (!out) {
+        PyBuffer_Release(&view);
+        return nullptr;
+    }
+    std::string& line = *self->chunk_line;
+    size_t i = 0;
+    bool ok = true;
+    while (ok && i < n && self->cstate != CS_DONE) {
+        switch (self->cstate) {
+            case CS_SIZE: {
+                const char* nl = (const char*)std::memchr(data + i, '\n', n - i);
+                if (!nl) {
+                    line.append(data + i, n - i);
+                    if (line.size() > 4096) {
+                        PyErr_SetString(PyExc_ValueError, "chunk size line too long");
+                        ok = false;
+                    }
+                    i = n;
+                    break;
+                }
+                line.append(data + i, (size_t)(nl - (data + i)));
+                i = (size_t)(nl - data) + 1;
+                size_t size;
+                if (!parse_chunk_size(line, size)) {
+                    PyErr_Format(PyExc_ValueError, "bad chunk size line %.40s", line.c_str());
+                    ok = false;
+                    break;
+                }
+                line.clear();
+                if (size == 0) {
+                    self->cstate = CS_TRAILER;
+                } else {
+                    self->cremain = size;
+                    self->cstate = CS_DATA;
+                }
+                break;
+            }
+            case CS_DATA: {
+                size_t take = self->cremain < n - i ? self->cremain : n - i;
+                ok = process_segment(self, data + i, take, out);
+                i += take;
+                self->cremain -= take;
+                if (self->cremain == 0) self->cstate = CS_DATA_END;
+                break;
+            }
+            case CS_DATA_END: {
+                const char* nl = (const char*)std::memchr(data + i, '\n', n - i);
+                if (!nl) {
+                    i = n;
+                    break;
+                }
+                i = (size_t)(nl - data) + 1;
+                self->cstate = CS_SIZE;
+                break;
+            }
+            case CS_TRAILER: {
+                const char* nl = (const char*)std::memchr(data + i, '\n', n - i);
+                if (!nl) {
+                    line.append(data + i, n - i);
+                    i = n;
+                    break;
+                }
+                line.append(data + i, (size_t)(nl - (data + i)));
+                i = (size_t)(nl - data) + 1;
+                bool empty = line.empty() || (line.size() == 1 && line[0] == '\r');
+                line.clear();
+                if (empty) self->cstate = CS_DONE;
+                break;
+            }
+        }
     }
     PyBuffer_Release(&view);
     if (!ok) {
@@ -976,8 +1092,15 @@ PyObject* Decoder_feed(DecoderObject* self, PyObject* arg) {
     return out;
 }
 
+PyObject* Decoder_body_done(DecoderObject* self, PyObject*) {
+    return PyBool_FromLong(self->cstate == CS_DONE);
+}
+
 PyObject* Decoder_reset(DecoderObject* self, PyObject*) {
     self->partial->clear();
+    self->chunk_line->clear();
+    self->cstate = CS_SIZE;
+    self->cremain = 0;
     Py_RETURN_NONE;
 }
 
@@ -1100,7 +1223,10 @@ PyObject* Decoder_stats(DecoderObject* self, PyObject*) {
 
 PyMethodDef Decoder_methods[] = {
     {"feed", (PyCFunction)Decoder_feed, METH_O, "feed(bytes) -> list of event tuples"},
-    {"reset", (PyCFunction)Decoder_reset, METH_NOARGS, "drop any partial line"},
+    {"feed_chunked", (PyCFunction)Decoder_feed_chunked, METH_O,
+     "feed_chunked(bytes) -> events; input keeps its HTTP chunked framing"},
+    {"body_done", (PyCFunction)Decoder_body_done, METH_NOARGS, "True after the terminating 0-size chunk"},
+    {"reset", (PyCFunction)Decoder_reset, METH_NOARGS, "drop partial line and chunk state"},
     {"decode_list", (PyCFunction)Decoder_decode_list, METH_O, "decode_list(body) -> (rv, continue, events)"},
     {"core", (PyCFunction)Decoder_core, METH_O, "core(event) -> payload core bytes"},
     {"core_from_summary", (PyCFunction)Decoder_core_from_summary, METH_VARARGS,

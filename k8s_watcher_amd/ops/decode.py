@@ -33,13 +33,19 @@ ADDED, MODIFIED, DELETED, BOOKMARK, ERROR, INVALID = (
     "ADDED", "MODIFIED", "DELETED", "BOOKMARK", "ERROR", "INVALID")
 
 
+def _s(v: Any) -> Optional[str]:
+    """Identity fields are strings; anything else (null, numbers) reads as None."""
+    return v if isinstance(v, str) else None
+
+
 def event_from_object(etype: str, obj: Dict[str, Any]) -> tuple:
     if etype == ERROR:
         return (ERROR, None, None, None, None, None, False, None, obj)
     md = obj.get("metadata") or {}
     st = obj.get("status")
-    return (etype, md.get("uid"), md.get("namespace"), md.get("name"), md.get("resourceVersion"),
-            st.get("phase") if st is not None else None, st is not None, obj, None)
+    return (etype, _s(md.get("uid")), _s(md.get("namespace")), _s(md.get("name")),
+            _s(md.get("resourceVersion")), _s(st.get("phase")) if st is not None else None,
+            st is not None, obj, None)
 
 
 class PyDecoder:
@@ -49,9 +55,54 @@ class PyDecoder:
         self.environment = environment
         self.state_format = state_format
         self._partial = b""
+        self._cbuf = b""
+        self._cremain = 0
+        self._cstate = 0  # 0 size line, 1 data, 2 data CRLF, 3 trailers, 4 done
 
     def reset(self) -> None:
         self._partial = b""
+        self._cbuf = b""
+        self._cremain = 0
+        self._cstate = 0
+
+    def body_done(self) -> bool:
+        return self._cstate == 4
+
+    def feed_chunked(self, data: bytes) -> List[tuple]:
+        """Like :meth:`feed` for input that still carries HTTP chunked framing."""
+        buf = self._cbuf + data if self._cbuf else data
+        self._cbuf = b""
+        out: List[tuple] = []
+        i, n = 0, len(buf)
+        while i < n and self._cstate != 4:
+            st = self._cstate
+            if st == 1:
+                take = min(self._cremain, n - i)
+                out.extend(self.feed(buf[i:i + take]))
+                i += take
+                self._cremain -= take
+                if self._cremain == 0:
+                    self._cstate = 2
+                continue
+            nl = buf.find(b"\n", i)
+            if nl < 0:
+                if st != 2:
+                    self._cbuf = buf[i:]
+                break
+            line = buf[i:nl].rstrip(b"\r")
+            i = nl + 1
+            if st == 0:
+                size = int(line.split(b";", 1)[0].strip(), 16)
+                if size == 0:
+                    self._cstate = 3
+                else:
+                    self._cremain = size
+                    self._cstate = 1
+            elif st == 2:
+                self._cstate = 0
+            elif st == 3 and not line:
+                self._cstate = 4
+        return out
 
     def feed(self, data: bytes) -> List[tuple]:
         buf = self._partial + data if self._partial else data

@@ -99,6 +99,8 @@ class NativeDecoder:
         self.state_format = state_format
         # bind C methods directly: no Python frame per call
         self.feed = d.feed
+        self.feed_chunked = d.feed_chunked
+        self.body_done = d.body_done
         self.reset = d.reset
         self.decode_list = d.decode_list
         self.core = d.core

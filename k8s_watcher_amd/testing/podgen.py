@@ -25,6 +25,11 @@ NAMESPACES_DEFAULT = ["default", "kube-system", "production", "monitoring",
                       "staging", "batch", "ml-train", "ingress"]
 
 
+def _clone(obj: Any) -> Any:
+    """Deep copy of a JSON document (several times faster than ``copy.deepcopy``)."""
+    return json.loads(json.dumps(obj))
+
+
 def _ts(offset_s: float) -> str:
     return (BASE_TIME + _dt.timedelta(seconds=offset_s)).strftime("%Y-%m-%dT%H:%M:%SZ")
 
@@ -136,7 +141,7 @@ class PodFactory:
 
     # ----------------------------------------------------------------- lifecycle
     def scheduled(self, pod: Dict[str, Any]) -> Dict[str, Any]:
-        p = copy.deepcopy(pod)
+        p = _clone(pod)
         n = self.counter
         p["spec"]["nodeName"] = f"mi355x-node-{n % 16:02d}"
         t0 = 1.0
@@ -164,7 +169,7 @@ class PodFactory:
         return p
 
     def running(self, pod: Dict[str, Any]) -> Dict[str, Any]:
-        p = copy.deepcopy(pod) if "conditions" in (pod.get("status") or {}) else self.scheduled(pod)
+        p = _clone(pod) if "conditions" in (pod.get("status") or {}) else self.scheduled(pod)
         st = p["status"]
         st["phase"] = "Running"
         n = self.counter
@@ -185,7 +190,7 @@ class PodFactory:
         return p
 
     def terminated(self, pod: Dict[str, Any], failed: bool = False) -> Dict[str, Any]:
-        p = self.running(pod) if (pod.get("status") or {}).get("phase") != "Running" else copy.deepcopy(pod)
+        p = self.running(pod) if (pod.get("status") or {}).get("phase") != "Running" else _clone(pod)
         st = p["status"]
         st["phase"] = "Failed" if failed else "Succeeded"
         for c in st["conditions"]:
@@ -203,7 +208,7 @@ class PodFactory:
         return p
 
     def deleting(self, pod: Dict[str, Any]) -> Dict[str, Any]:
-        p = copy.deepcopy(pod)
+        p = _clone(pod)
         p["metadata"]["deletionTimestamp"] = _ts(90)
         p["metadata"]["deletionGracePeriodSeconds"] = 0
         return p

@@ -63,10 +63,16 @@ class Template:
 
 
 class ReplayServer:
-    def __init__(self, template: Template) -> None:
+    def __init__(self, template: Template, prerender: int = 0) -> None:
         self.t = template
         self.watchers: List[asyncio.StreamWriter] = []
         self.rv = 1000
+        # Whole steps rendered ahead of time so that, during a timed step, this
+        # process only issues send() calls and can never be the bottleneck.
+        self.rendered = {k: self.t.render(k, 0, len(self.t), self.rv_base(k)) for k in range(prerender)}
+
+    def rv_base(self, step: int) -> int:
+        return 10_000_000 + step * len(self.t)
 
     async def handle(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
         try:
@@ -105,8 +111,16 @@ class ReplayServer:
 
     async def send(self, step: int, rate: Optional[float] = None, count: Optional[int] = None) -> int:
         n = len(self.t) if count is None else min(count, len(self.t))
-        rv_base = 10_000_000 + step * len(self.t)
-        if rate:
+        rv_base = self.rv_base(step)
+        pre = self.rendered.pop(step, None)
+        if pre is not None and count is None:
+            view = memoryview(pre)
+            piece = 1 << 22
+            for a in range(0, len(view), piece):
+                for w in list(self.watchers):
+                    w.write(view[a:a + piece])
+                    await w.drain()
+        elif rate:
             t0 = time.monotonic()
             for i in range(n):
                 data = self.t.render(step, i, i + 1, rv_base)
@@ -128,7 +142,7 @@ class ReplayServer:
 
 async def amain(args) -> None:
     tmpl = Template(args.pods_per_step, args.seed, args.namespaces.split(",") if args.namespaces else None)
-    srv = ReplayServer(tmpl)
+    srv = ReplayServer(tmpl, args.prerender)
     server = await asyncio.start_server(srv.handle, "127.0.0.1", args.port)
     port = server.sockets[0].getsockname()[1]
     print(f"READY {port} {len(tmpl)}", flush=True)
@@ -163,6 +177,7 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--pods-per-step", type=int, default=10000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--namespaces", default=None)
+    ap.add_argument("--prerender", type=int, default=0, help="render steps [0, N) before READY")
     asyncio.run(amain(ap.parse_args(argv)))
 
 
