@@ -1,0 +1,137 @@
+"""Single-request clusterapi clients.
+
+Reference: ``ClusterApiClient`` (``/root/reference/watcher/clusterapi_client.py:6-61``)
+— a ``requests.Session`` POSTing ``{base}/api/pods/update``. The same public
+surface is kept (``update_pod_status(pod_data) -> bool``,
+``health_check() -> bool``, bearer-key header, the same log lines) with the
+reference's defects fixed: the ``timeout`` is honoured, the
+endpoint paths come from ``clusterapi.endpoints``, any 2xx is success and
+``clusterapi.retry`` is applied with exponential backoff. The constructor
+accepts the three positional arguments the reference's factory passes
+(``pod_watcher.py:108``), which its own ``__init__`` rejected.
+
+:class:`ClusterApiClient` is synchronous (``requests``);
+:class:`AsyncClusterApiClient` runs on the framework's asyncio HTTP client.
+For high event rates use :class:`k8s_watcher_amd.parallel.notifier.NotifierPool`.
+"""
+
+from __future__ import annotations
+
+import json
+import logging
+import time
+from typing import Any, Dict, Optional
+
+from ..net.http import HttpClient, HttpError
+from ..utils.config import RetryPolicy
+from ..utils.logsetup import NOTIFIER_LOGGER
+
+RETRYABLE = frozenset({408, 425, 429, 500, 502, 503, 504})
+
+
+class _Common:
+    def __init__(self, base_url: str, api_key: Optional[str] = None, timeout: float = 30.0,
+                 pod_update: str = "/api/pods/update", health: str = "/health",
+                 retry: Optional[RetryPolicy] = None) -> None:
+        self.base_url = base_url.rstrip("/")
+        self.api_key = api_key
+        self.timeout = timeout
+        self.pod_update = pod_update
+        self.health = health
+        self.retry = retry or RetryPolicy(max_attempts=1, delay_seconds=0.0)
+        self.logger = logging.getLogger(NOTIFIER_LOGGER)
+        self.headers = {"Content-Type": "application/json"}
+        if api_key:
+            self.headers["Authorization"] = f"Bearer {api_key}"
+
+    @property
+    def endpoint(self) -> str:
+        return f"{self.base_url}{self.pod_update}"
+
+    @classmethod
+    def from_settings(cls, c) -> "_Common":
+        return cls(c.base_url, c.api_key or None, c.timeout, c.pod_update, c.health, c.retry)
+
+
+class ClusterApiClient(_Common):
+    """Synchronous client (``requests``), API-compatible with the reference."""
+
+    def __init__(self, *args: Any, **kwargs: Any) -> None:
+        super().__init__(*args, **kwargs)
+        import requests
+        self._requests = requests
+        self.session = requests.Session()
+        self.session.headers.update(self.headers)
+
+    def update_pod_status(self, pod_data: Dict[str, Any]) -> bool:
+        ep = self.endpoint
+        self.logger.info(f"Calling clusterapi: {ep}")
+        if self.logger.isEnabledFor(logging.DEBUG):
+            self.logger.debug(f"Pod data: {json.dumps(pod_data, indent=2)}")
+        body = json.dumps(pod_data).encode("utf-8")
+        for attempt in range(1, max(1, self.retry.max_attempts) + 1):
+            status = None
+            try:
+                resp = self.session.post(ep, data=body, timeout=self.timeout)
+                status = resp.status_code
+                if 200 <= status < 300:
+                    self.logger.info(f"Successfully updated pod data for {pod_data.get('name', 'unknown')}")
+                    return True
+                self.logger.error(f"Failed to update pod data. Status: {status}, Response: {resp.text}")
+            except self._requests.exceptions.ConnectionError:
+                self.logger.error(f"Connection error: Unable to connect to clusterapi at {ep}")
+            except self._requests.exceptions.Timeout:
+                self.logger.error(f"Timeout error: Request to {ep} timed out")
+            except Exception as exc:  # noqa: BLE001 - parity
+                self.logger.error(f"Unexpected error calling clusterapi: {exc}")
+                return False
+            if status is not None and status not in RETRYABLE:
+                return False
+            if attempt < self.retry.max_attempts:
+                time.sleep(self.retry.delay(attempt))
+        return False
+
+    def health_check(self) -> bool:
+        try:
+            resp = self.session.get(f"{self.base_url}{self.health}", timeout=min(5.0, self.timeout))
+            return 200 <= resp.status_code < 300
+        except Exception:  # noqa: BLE001 - parity: any failure -> False
+            return False
+
+
+class AsyncClusterApiClient(_Common):
+    """Same API, ``async``, over the framework's keep-alive HTTP client."""
+
+    def __init__(self, *args: Any, ssl_context=None, **kwargs: Any) -> None:
+        super().__init__(*args, **kwargs)
+        self.http = HttpClient(self.base_url, ssl_context, headers=self.headers, timeout=self.timeout)
+
+    async def update_pod_status(self, pod_data: Dict[str, Any]) -> bool:
+        import asyncio
+        ep = self.endpoint
+        body = json.dumps(pod_data).encode("utf-8")
+        for attempt in range(1, max(1, self.retry.max_attempts) + 1):
+            status = None
+            try:
+                resp = await self.http.request("POST", self.pod_update, body=body)
+                status = resp.status
+                if resp.ok:
+                    return True
+                self.logger.error(f"Failed to update pod data. Status: {status}, Response: {resp.text()}")
+            except HttpError as exc:
+                self.logger.error(f"Connection error: Unable to connect to clusterapi at {ep} ({exc})")
+            if status is not None and status not in RETRYABLE:
+                return False
+            if attempt < self.retry.max_attempts:
+                await asyncio.sleep(self.retry.delay(attempt))
+        return False
+
+    async def health_check(self) -> bool:
+        try:
+            resp = await self.http.request("GET", self.health, timeout=min(5.0, self.timeout))
+            return resp.ok
+        except Exception:  # noqa: BLE001
+            return False
+
+    async def close(self) -> None:
+        await self.http.close()

@@ -160,6 +160,7 @@ class _Conn(asyncio.Protocol):
             failed = list(self.queue)
             self.queue.clear()
             for req in failed:
+                req.attempts += 1  # a refused connection counts as an attempt
                 pool._failed(req, None, f"Connection error: Unable to connect to clusterapi at "
                                         f"{pool.endpoint_url} ({exc.__class__.__name__})")
             if self.queue:

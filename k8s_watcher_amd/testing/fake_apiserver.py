@@ -143,9 +143,10 @@ class FakeApiServer:
         self._bm_task: Optional[asyncio.Task] = None
 
     # ------------------------------------------------------------------ lifecycle
-    async def start(self, host: str = "127.0.0.1", port: int = 0) -> int:
+    async def start(self, host: str = "127.0.0.1", port: int = 0, ssl_context=None) -> int:
         self.loop = asyncio.get_running_loop()
-        self.server = await asyncio.start_server(self._handle, host, port, limit=1 << 20)
+        self.scheme = "https" if ssl_context is not None else "http"
+        self.server = await asyncio.start_server(self._handle, host, port, limit=1 << 20, ssl=ssl_context)
         self.port = self.server.sockets[0].getsockname()[1]
         if self.bookmark_interval:
             self._bm_task = asyncio.ensure_future(self._bookmark_loop())
@@ -153,7 +154,7 @@ class FakeApiServer:
 
     @property
     def url(self) -> str:
-        return f"http://127.0.0.1:{self.port}"
+        return f"{getattr(self, 'scheme', 'http')}://127.0.0.1:{self.port}"
 
     async def stop(self) -> None:
         if self._bm_task:
@@ -443,17 +444,19 @@ class FakeApiServer:
 class ServerThread:
     """Run a :class:`FakeApiServer` on its own event loop in a daemon thread."""
 
-    def __init__(self, server: FakeApiServer, host: str = "127.0.0.1", port: int = 0) -> None:
+    def __init__(self, server: FakeApiServer, host: str = "127.0.0.1", port: int = 0,
+                 ssl_context=None) -> None:
         self.server = server
         self.loop = asyncio.new_event_loop()
         self._ready = threading.Event()
         self._host = host
         self._port = port
+        self._ssl = ssl_context
         self.thread = threading.Thread(target=self._run, daemon=True)
 
     def _run(self) -> None:
         asyncio.set_event_loop(self.loop)
-        self.loop.run_until_complete(self.server.start(self._host, self._port))
+        self.loop.run_until_complete(self.server.start(self._host, self._port, self._ssl))
         self._ready.set()
         self.loop.run_forever()
 

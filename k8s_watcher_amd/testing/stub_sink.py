@@ -52,6 +52,7 @@ class SinkState:
         self.fail_next: List[int] = []
         self.rng = random.Random(seed)
         self.received: List[Tuple[int, bytes]] = []
+        self.heads: List[bytes] = []
         self.count = 0
         self.failed = 0
         self.health_checks = 0
@@ -134,6 +135,7 @@ class _SinkProtocol(asyncio.Protocol):
             st.count += 1
             if st.record:
                 st.received.append((now, body))
+                st.heads.append(head)
             responses.append(_OK if st.success_status == 200 else _resp(st.success_status))
         if pos:
             del buf[:pos]

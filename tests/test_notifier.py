@@ -1,0 +1,251 @@
+"""clusterapi notifier pool: success codes, retries,
+timeouts, per-pod ordering, superseding, coalescing and backpressure."""
+
+import asyncio
+import json
+import random
+
+import pytest
+
+from conftest import run
+from k8s_watcher_amd.metrics import Metrics
+from k8s_watcher_amd.models.payload import build_core
+from k8s_watcher_amd.parallel.notifier import NotifierPool
+from k8s_watcher_amd.testing.stub_sink import StubSink
+from k8s_watcher_amd.utils.config import ClusterApiSettings, NotifierPoolSettings, RetryPolicy
+
+TS = "2025-01-01T00:00:00.000001"
+
+
+def settings(url, **kw):
+    pool = NotifierPoolSettings(connections=kw.pop("connections", 4), pipeline_depth=kw.pop("depth", 1),
+                                queue_size=kw.pop("queue_size", 1000), coalesce=kw.pop("coalesce", False))
+    retry = RetryPolicy(kw.pop("attempts", 3), kw.pop("delay", 0.01), 2.0, 1.0, 0.0)
+    return ClusterApiSettings(base_url=url, pool=pool, retry=retry, **kw)
+
+
+def core(uid, phase="Running", name=None):
+    pod = {"metadata": {"name": name or f"pod-{uid}", "namespace": "default", "uid": uid},
+           "status": {"phase": phase}}
+    return build_core(pod, "production")
+
+
+async def with_pool(sink_kwargs=None, **kw):
+    sink = StubSink(**(sink_kwargs or {}))
+    await sink.start()
+    m = Metrics(record_samples=True)
+    pool = NotifierPool(settings(sink.url, **kw), m)
+    return sink, pool, m
+
+
+async def close(sink, pool):
+    await pool.close()
+    await sink.stop()
+
+
+def test_delivers_with_headers_and_latency():
+    async def body():
+        sink, pool, m = await with_pool(api_key="k3y")
+        for i in range(20):
+            pool.submit(f"u{i}", "ADDED", "default", f"p{i}", core(f"u{i}"), 0, TS)
+        pool.flush()
+        assert await pool.drain(5)
+        heads = list(sink.state.heads)
+        got = sink.state.payloads()
+        await close(sink, pool)
+        return heads, got, m
+
+    heads, got, m = run(body())
+    assert len(got) == 20 and m.c["notify_delivered"] == 20
+    assert all(b"Authorization: Bearer k3y" in h for h in heads)
+    assert all(h.startswith(b"POST /api/pods/update HTTP/1.1") for h in heads)
+    assert got[0]["event_timestamp"] == TS and got[0]["event_type"] == "ADDED"
+    assert m.latency.n == 20
+
+
+@pytest.mark.parametrize("status", [201, 204])
+def test_any_2xx_is_success(status):
+    async def body():
+        sink, pool, m = await with_pool({"success_status": status})
+        pool.submit("u", "ADDED", "default", "p", core("u"), 0, TS)
+        pool.flush()
+        await pool.drain(5)
+        await close(sink, pool)
+        return m
+
+    m = run(body())
+    assert m.c["notify_delivered"] == 1 and m.c["notify_failed"] == 0
+
+
+def test_5xx_retried_4xx_not():
+    async def body():
+        sink, pool, m = await with_pool()
+        sink.state.fail_next = [500, 503]
+        pool.submit("a", "ADDED", "default", "a", core("a"), 0, TS)
+        pool.flush()
+        await pool.drain(5)
+        sink.state.fail_next = [400]
+        pool.submit("b", "ADDED", "default", "b", core("b"), 0, TS)
+        pool.flush()
+        await pool.drain(5)
+        names = [p["name"] for p in sink.state.payloads()]
+        await close(sink, pool)
+        return names, m
+
+    names, m = run(body())
+    assert names == ["pod-a"]
+    assert m.c["notify_retried"] == 2 and m.c["notify_failed"] == 1 and m.c["notify_delivered"] == 1
+
+
+def test_gives_up_after_max_attempts():
+    async def body():
+        sink, pool, m = await with_pool({"fail_rate": 1.0}, attempts=3)
+        pool.submit("a", "ADDED", "default", "a", core("a"), 0, TS)
+        pool.flush()
+        assert await pool.drain(5)
+        await close(sink, pool)
+        return m, sink.state.failed
+
+    m, failed = run(body())
+    assert failed == 3 and m.c["notify_failed"] == 1 and m.c["notify_retried"] == 2
+
+
+def test_timeout_aborts_and_retries():
+    async def body():
+        sink, pool, m = await with_pool({"latency": 0.6}, timeout=0.2, attempts=2, delay=0.3)
+        pool.submit("a", "ADDED", "default", "a", core("a"), 0, TS)
+        pool.flush()
+        await asyncio.sleep(0.35)
+        sink.state.latency = 0.0  # clusterapi recovers
+        assert await pool.drain(5)
+        await close(sink, pool)
+        return m
+
+    m = run(body())
+    assert m.c["notify_retried"] == 1 and m.c["notify_delivered"] == 1
+
+
+def test_stale_retry_is_superseded():
+    async def body():
+        sink, pool, m = await with_pool(connections=1, delay=0.2)
+        sink.state.fail_next = [503]
+        pool.submit("u", "MODIFIED", "default", "p", core("u", "Running"), 0, TS)
+        pool.flush()
+        await asyncio.sleep(0.05)  # first attempt failed, retry scheduled in 0.2 s
+        pool.submit("u", "MODIFIED", "default", "p", core("u", "Succeeded"), 0, TS)
+        pool.flush()
+        await pool.drain(5)
+        phases = [p["status"]["phase"] for p in sink.state.payloads()]
+        await close(sink, pool)
+        return phases, m
+
+    phases, m = run(body())
+    assert phases == ["Succeeded"]  # the stale Running body never reaches clusterapi
+    assert m.c["notify_superseded"] == 1
+
+
+def test_coalesce_replaces_unsent_body():
+    async def body():
+        sink, pool, m = await with_pool(coalesce=True, connections=1)
+        for ph in ("Pending", "Running", "Succeeded"):
+            pool.submit("u", "MODIFIED", "default", "p", core("u", ph), 0, TS)
+        pool.flush()
+        await pool.drain(5)
+        phases = [p["status"]["phase"] for p in sink.state.payloads()]
+        await close(sink, pool)
+        return phases, m
+
+    phases, m = run(body())
+    # the connection is not up at submit time, so all three coalesce into one request
+    assert phases == ["Succeeded"] and m.c["notify_coalesced"] == 2
+
+
+@pytest.mark.parametrize("depth", [1, 8])
+def test_per_pod_order_under_random_failures(depth):
+    rng = random.Random(3)
+    order = ["Pending", "Running", "Succeeded"]
+
+    async def body():
+        sink, pool, m = await with_pool({"fail_rate": 0.2, "fail_status": 503, "seed": 5},
+                                        connections=4, depth=depth, attempts=8, delay=0.005)
+        uids = [f"u{i}" for i in range(40)]
+        steps = {u: 0 for u in uids}
+        while any(s < 3 for s in steps.values()):
+            u = rng.choice([u for u, s in steps.items() if s < 3])
+            pool.submit(u, "MODIFIED", "default", u, core(u, order[steps[u]]), 0, TS)
+            steps[u] += 1
+            if rng.random() < 0.3:
+                pool.flush()
+                await asyncio.sleep(0)
+        pool.flush()
+        assert await pool.drain(10)
+        got = sink.state.payloads()
+        await close(sink, pool)
+        return got, m
+
+    got, m = run(body())
+    seen = {}
+    for p in got:
+        idx = order.index(p["status"]["phase"])
+        assert idx >= seen.get(p["uid"], -1), "an older state overwrote a newer one"
+        seen[p["uid"]] = idx
+    assert all(v == 2 for v in seen.values()) and len(seen) == 40  # final state always delivered
+    assert m.c["notify_failed"] == 0
+
+
+def test_backpressure_signals():
+    flips = []
+
+    async def body():
+        sink = StubSink(latency=0.05)
+        await sink.start()
+        pool = NotifierPool(settings(sink.url, queue_size=8, connections=2), Metrics(),
+                            on_saturation=flips.append)
+        for i in range(20):
+            pool.submit(f"u{i}", "ADDED", "default", "p", core(f"u{i}"), 0, TS)
+        pool.flush()
+        assert pool.saturated
+        await pool.drain(10)
+        await close(sink, pool)
+
+    run(body())
+    assert flips == [True, False]
+
+
+def test_unreachable_sink_then_recovery():
+    async def body():
+        import socket
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        m = Metrics()
+        pool = NotifierPool(settings(f"http://127.0.0.1:{port}", attempts=2, delay=0.01), m)
+        pool.submit("a", "ADDED", "default", "a", core("a"), 0, TS)
+        pool.flush()
+        assert await pool.drain(5)
+        failed = m.c["notify_failed"]
+        sink = StubSink()
+        await sink.start(port=port)
+        pool.submit("b", "ADDED", "default", "b", core("b"), 0, TS)
+        pool.flush()
+        assert await pool.drain(10)
+        n = sink.state.count
+        await close(sink, pool)
+        return failed, n
+
+    failed, n = run(body())
+    assert failed == 1 and n == 1
+
+
+def test_health_check():
+    async def body():
+        sink, pool, m = await with_pool()
+        ok = await pool.health_check()
+        await close(sink, pool)
+        bad = NotifierPool(settings("http://127.0.0.1:1"), Metrics())
+        nok = await bad.health_check(timeout=1)
+        await bad.close()
+        return ok, nok
+
+    assert run(body()) == (True, False)

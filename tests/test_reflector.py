@@ -1,0 +1,289 @@
+"""Watch robustness (BASELINE config #5): resume, 410 relist,
+bookmarks, retries, checkpoint restart — each asserting exactly-once delivery."""
+
+import asyncio
+import collections
+
+import pytest
+
+from conftest import run
+from k8s_watcher_amd.engine.reflector import WatchFailed
+from k8s_watcher_amd.engine.service import WatcherService
+from k8s_watcher_amd.kube.kubeconfig import KubeEndpoint
+from k8s_watcher_amd.metrics import Metrics
+from k8s_watcher_amd.testing.fake_apiserver import FakeApiServer
+from k8s_watcher_amd.testing.podgen import PodFactory
+from k8s_watcher_amd.testing.stub_sink import StubSink
+from k8s_watcher_amd.utils.config import deep_merge, load_settings
+
+
+class Stack:
+    def __init__(self, environment="staging", overrides=None, server_kwargs=None, sink_kwargs=None):
+        self.environment = environment
+        self.overrides = overrides or {}
+        self.server_kwargs = server_kwargs or {}
+        self.sink_kwargs = sink_kwargs or {}
+        self.factory = PodFactory(seed=21, namespaces=["default", "kube-system", "batch"])
+
+    async def __aenter__(self):
+        self.srv = FakeApiServer(**self.server_kwargs)
+        await self.srv.start()
+        self.sink = StubSink(**self.sink_kwargs)
+        await self.sink.start()
+        return self
+
+    def service(self, extra=None):
+        ov = {"clusterapi": {"base_url": self.sink.url, "retry": {"delay_seconds": 0.01, "max_attempts": 5},
+                             "health_check_on_start": False},
+              "watcher": {"retry": {"delay_seconds": 0.01, "max_attempts": 0}}}
+        ov = deep_merge(deep_merge(ov, self.overrides), extra or {})
+        self.settings = load_settings(self.environment, overrides=ov)
+        self.svc = WatcherService(self.settings, endpoint=KubeEndpoint(server=self.srv.url), metrics=Metrics(True))
+        return self.svc
+
+    async def settle(self, n, timeout=10):
+        await self.sink.state.wait_for(n, timeout)
+        await asyncio.sleep(0.05)
+        await self.svc.notifier.drain(5)
+
+    def delivered(self):
+        return [(p["uid"], p["event_type"], p["status"]["phase"]) for p in self.sink.state.payloads()]
+
+    async def __aexit__(self, *exc):
+        if getattr(self, "svc", None) is not None:
+            self.svc.stop()
+            await self.svc.shutdown()
+        await self.sink.stop()
+        await self.srv.stop()
+
+
+def lifecycle_apply(st, n_pods):
+    evs = []
+    for _ in range(n_pods):
+        for et, obj in st.factory.lifecycle():
+            st.srv.apply(et, obj)
+            evs.append((obj["metadata"]["uid"], et))
+    return evs
+
+
+def assert_exactly_once(delivered, expected):
+    assert collections.Counter((u, t) for u, t, _ in delivered) == collections.Counter(expected)
+
+
+def test_resume_after_connection_drop_no_loss_no_dup():
+    async def body():
+        async with Stack() as st:
+            svc = st.service()
+            await svc.start()
+            first = lifecycle_apply(st, 5)
+            await st.settle(len(first))
+            st.srv.drop_connections()  # simulated API-server restart, history kept
+            second = lifecycle_apply(st, 5)
+            await st.settle(len(first) + len(second))
+            assert_exactly_once(st.delivered(), first + second)
+            assert svc.metrics.c["relists"] == 1  # only the initial list
+            assert svc.metrics.c["expired_410"] == 0
+
+    run(body())
+
+
+@pytest.mark.parametrize("as_http_status", [False, True])
+def test_410_relists_and_diffs_against_cache(as_http_status):
+    async def body():
+        async with Stack(server_kwargs={"expired_as_http_status": as_http_status}) as st:
+            f = st.factory
+            svc = st.service()
+            await svc.start()
+            keep = [st.srv.create(f.running(f.new_pod())) for _ in range(3)]
+            doomed = st.srv.create(f.running(f.new_pod()))
+            changing = st.srv.create(f.running(f.new_pod()))
+            await st.settle(5)
+            # while the watch is down: etcd compacts past our resourceVersion
+            st.srv.drop_connections()
+            st.srv.delete("default" if False else doomed["metadata"]["namespace"], doomed["metadata"]["name"])
+            st.srv.update(f.terminated(changing))
+            newcomer = st.srv.create(f.running(f.new_pod()))
+            st.srv.compact()
+            st.srv.expire_watches()
+            await st.settle(8)
+            got = st.delivered()
+            assert len(got) == 8
+            tail = {(u, t) for u, t, _ in got[5:]}
+            assert tail == {(doomed["metadata"]["uid"], "DELETED"), (changing["metadata"]["uid"], "MODIFIED"),
+                            (newcomer["metadata"]["uid"], "ADDED")}
+            assert svc.metrics.c["expired_410"] >= 1 and svc.metrics.c["relists"] == 2
+            # unchanged pods were not re-notified
+            assert [u for u, _, _ in got].count(keep[0]["metadata"]["uid"]) == 1
+
+    run(body())
+
+
+def test_bookmark_advances_resume_point():
+    async def body():
+        async with Stack() as st:
+            f = st.factory
+            svc = st.service()
+            await svc.start()
+            st.srv.create(f.new_pod())
+            await st.settle(1)
+            # traffic the watcher does not see (other scope) moves the RV on; a bookmark reports it
+            st.srv.rv += 500
+            st.srv.emit_bookmark()
+            await asyncio.sleep(0.1)
+            rv = svc.reflectors[0].rv
+            assert rv == str(st.srv.rv)
+            assert svc.metrics.c["bookmarks"] >= 1
+            st.srv.compact()  # history before the bookmark is gone; resume must not 410
+            st.srv.drop_connections()
+            st.srv.create(f.new_pod())
+            await st.settle(2)
+            assert svc.metrics.c["expired_410"] == 0
+
+    run(body())
+
+
+def test_server_timeout_seconds_resumes():
+    async def body():
+        async with Stack(overrides={"watcher": {"watch_timeout_seconds": 1}}) as st:
+            svc = st.service()
+            await svc.start()
+            await asyncio.sleep(1.4)  # first watch ends server-side
+            evs = lifecycle_apply(st, 2)
+            await st.settle(len(evs))
+            assert_exactly_once(st.delivered(), evs)
+            assert svc.metrics.c["watch_restarts"] >= 1
+
+    run(body())
+
+
+def test_transient_api_errors_retry():
+    async def body():
+        async with Stack() as st:
+            st.srv.fail_requests(3, 500, "/api/v1/pods")
+            svc = st.service()
+            await svc.start()
+            evs = lifecycle_apply(st, 1)
+            await st.settle(len(evs))
+            assert_exactly_once(st.delivered(), evs)
+
+    run(body())
+
+
+def test_retry_budget_exhausted_is_fatal():
+    async def body():
+        async with Stack(overrides={"watcher": {"retry": {"max_attempts": 2}}}) as st:
+            svc = st.service()
+            await svc.start()
+            st.srv.fail_requests(50, 503, "/api/v1/pods")
+            st.srv.drop_connections()
+            with pytest.raises(WatchFailed):
+                await asyncio.wait_for(svc.wait(), 10)
+
+    run(body())
+
+
+def test_checkpoint_restart_exactly_once(tmp_path):
+    ck = str(tmp_path / "ckpt.json")
+
+    async def body():
+        async with Stack(overrides={"watcher": {"checkpoint": {"path": ck, "interval_seconds": 0.2}}}) as st:
+            f = st.factory
+            svc = st.service()
+            await svc.start()
+            pods = [st.srv.create(f.running(f.new_pod())) for _ in range(4)]
+            await st.settle(4)
+            svc.stop()
+            await svc.shutdown()
+            # watcher down: changes happen
+            st.srv.update(f.terminated(pods[0]))
+            st.srv.delete(pods[1]["metadata"]["namespace"], pods[1]["metadata"]["name"])
+            late = st.srv.create(f.running(f.new_pod()))
+            svc2 = st.service()
+            await svc2.start()
+            await st.settle(7)
+            got = st.delivered()
+            assert len(got) == 7, got
+            assert {(u, t) for u, t, _ in got[4:]} == {
+                (pods[0]["metadata"]["uid"], "MODIFIED"), (pods[1]["metadata"]["uid"], "DELETED"),
+                (late["metadata"]["uid"], "ADDED")}
+            assert svc2.metrics.c["relists"] == 0  # resumed straight from the checkpointed RV
+
+    run(body())
+
+
+def test_checkpoint_restart_after_compaction_diffs(tmp_path):
+    ck = str(tmp_path / "ckpt.json")
+
+    async def body():
+        async with Stack(overrides={"watcher": {"checkpoint": {"path": ck}}}) as st:
+            f = st.factory
+            svc = st.service()
+            await svc.start()
+            pods = [st.srv.create(f.running(f.new_pod())) for _ in range(4)]
+            await st.settle(4)
+            svc.stop()
+            await svc.shutdown()
+            st.srv.update(f.terminated(pods[2]))
+            st.srv.compact()
+            svc2 = st.service()
+            await svc2.start()
+            await st.settle(5)
+            got = st.delivered()
+            assert len(got) == 5
+            assert got[-1][:2] == (pods[2]["metadata"]["uid"], "MODIFIED")
+            assert svc2.metrics.c["expired_410"] == 1
+
+    run(body())
+
+
+def test_notify_on_phase_change():
+    async def body():
+        async with Stack(overrides={"watcher": {"notify_on": "phase_change"}}) as st:
+            f = st.factory
+            svc = st.service()
+            await svc.start()
+            p = st.srv.create(f.new_pod())          # ADDED Pending        -> notify
+            p = st.srv.update(f.scheduled(p))       # Pending -> Pending   -> suppressed
+            p = st.srv.update(f.running(p))         # Running              -> notify
+            p = st.srv.update(f.running(p))         # Running -> Running   -> suppressed
+            st.srv.delete(p["metadata"]["namespace"], p["metadata"]["name"])  # DELETED -> notify
+            await st.settle(3)
+            assert [t for _, t, _ in st.delivered()] == ["ADDED", "MODIFIED", "DELETED"]
+            assert svc.metrics.c["events_unchanged"] == 2
+
+    run(body())
+
+
+def test_initial_list_skip():
+    async def body():
+        async with Stack(overrides={"watcher": {"initial_list": "skip"}}) as st:
+            f = st.factory
+            for _ in range(3):
+                st.srv.create(f.running(f.new_pod()))
+            svc = st.service()
+            await svc.start()
+            new = st.srv.create(f.new_pod())
+            await st.settle(1)
+            assert [u for u, _, _ in st.delivered()] == [new["metadata"]["uid"]]
+            assert len(svc.pipeline.cache) == 4
+
+    run(body())
+
+
+def test_server_side_namespace_scope():
+    async def body():
+        async with Stack(environment="development",
+                         overrides={"watcher": {"namespace_scope": "server"}}) as st:
+            f = st.factory
+            svc = st.service()
+            await svc.start()
+            assert len(svc.reflectors) == 2
+            pods = [st.srv.create(f.new_pod()) for _ in range(6)]  # default/kube-system/batch round-robin
+            wanted = [p["metadata"]["uid"] for p in pods if p["metadata"]["namespace"] != "batch"]
+            await st.settle(len(wanted))
+            assert sorted(u for u, _, _ in st.delivered()) == sorted(wanted)
+            # the API server itself never sent the batch pods
+            assert svc.metrics.c["events_filtered_namespace"] == 0
+            assert any("/namespaces/default/pods" in t for _, t in st.srv.requests)
+
+    run(body())
