@@ -25,6 +25,7 @@ from ..ops.cache import CORE, MISSING, NAME, NS, PHASE, PodCache
 from ..ops.decode import (ADDED, BOOKMARK, DELETED, E_EXTRA, E_HAS_STATUS, E_NAME, E_NS, E_PHASE,
                           E_RV, E_TYPE, E_UID, MODIFIED)
 from ..ops.filters import TERMINAL_PHASES
+from ..parallel.shard import ShardFilter
 from ..utils.config import Settings
 from ..utils.logsetup import SERVICE_LOGGER
 from ..utils.timefmt import event_timestamp
@@ -47,6 +48,7 @@ class EventPipeline:
         self.phase_mode = w.notify_on == "phase_change"
         self.ts_mode = w.event_timestamp
         self.log_events_setting = w.log_events
+        self.shard = ShardFilter(w.shard)
         self.last_rv: Optional[str] = None
 
     @property
@@ -68,6 +70,7 @@ class EventPipeline:
         log_debug = log_events and log.isEnabledFor(logging.DEBUG)
         decoder = self.decoder
         submit = self.notifier.submit
+        shard = self.shard if self.shard.active else None
         ts = None
         for ev in events:
             et = ev[E_TYPE]
@@ -80,6 +83,11 @@ class EventPipeline:
                     ctrl.append(ev)
                 continue
             c["events_received"] += 1
+            if shard is not None and not shard.owns(ev[E_UID], ev[E_NS]):
+                if ev[E_RV]:
+                    self.last_rv = ev[E_RV]
+                c["events_other_shard"] += 1
+                continue
             uid = ev[E_UID]
             rv = ev[E_RV]
             if rv:
@@ -154,6 +162,8 @@ class EventPipeline:
         if not notify:
             for ev in out:
                 uid = ev[E_UID]
+                if self.shard.active and not self.shard.owns(uid, ev[E_NS]):
+                    continue
                 if ev[E_TYPE] == DELETED:
                     entries.pop(uid, None)
                 else:

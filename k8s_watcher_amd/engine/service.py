@@ -35,6 +35,7 @@ from ..net.http import HttpError
 from ..ops.cache import PodCache
 from ..ops.decode import make_decoder
 from ..parallel.notifier import NotifierPool, NullNotifier
+from ..parallel.shard import ShardFilter
 from ..utils.config import Settings
 from ..utils.logsetup import SERVICE_LOGGER
 from .checkpoint import load_checkpoint, save_checkpoint
@@ -140,8 +141,11 @@ class WatcherService:
             else:
                 self.log.warning("ClusterAPI health check failed, but continuing...")
         self.decoder = make_decoder(s.watcher.engine, s.environment, s.watcher.state_format)
-        scopes = (list(s.watcher.namespaces)
+        scopes = (ShardFilter(s.watcher.shard).namespaces(s.watcher.namespaces)
                   if s.watcher.namespace_scope == "server" and s.watcher.namespaces else [None])
+        if s.watcher.shard.count > 1:
+            self.log.info(f"Shard {s.watcher.shard.index}/{s.watcher.shard.count} "
+                          f"(key={s.watcher.shard.key}); watch scopes: {[x or '*' for x in scopes]}")
         cache = PodCache()
         saved_rvs = {}
         ck = s.watcher.checkpoint.path

@@ -26,6 +26,7 @@ COUNTERS = (
     "events_filtered_namespace",
     "events_unchanged",     # dropped by notify_on=phase_change
     "events_invalid",
+    "events_other_shard",
     "bookmarks",
     "notify_submitted",
     "notify_delivered",

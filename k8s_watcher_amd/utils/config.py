@@ -259,6 +259,16 @@ class WatcherSettings:
     event_timestamp: str = "local"  # local | utc
     log_events: Optional[bool] = None  # None = follow log level (parity)
     checkpoint: CheckpointSettings = field(default_factory=CheckpointSettings)
+    shard: "ShardSettings" = field(default_factory=lambda: ShardSettings())
+
+
+@dataclass
+class ShardSettings:
+    """Horizontal split of the pod space over ``count`` watcher processes."""
+
+    count: int = 1
+    index: int = 0
+    key: str = "namespace"  # namespace | uid
 
 
 @dataclass
@@ -286,6 +296,18 @@ def _retry(block: Any, key: str, default: RetryPolicy, min_attempts: int = 1) ->
         max_delay_seconds=_as_float(block.get("max_delay_seconds", default.max_delay_seconds), f"{key}.max_delay_seconds"),
         jitter=_as_float(block.get("jitter", default.jitter), f"{key}.jitter"),
     )
+
+
+def _shard(block: Dict[str, Any]) -> ShardSettings:
+    """``watcher.shard`` with ``$K8S_WATCHER_SHARD_INDEX/_COUNT`` taking precedence
+    (set per process by :mod:`k8s_watcher_amd.parallel.launch`)."""
+    count = os.environ.get("K8S_WATCHER_SHARD_COUNT", block.get("count", 1))
+    index = os.environ.get("K8S_WATCHER_SHARD_INDEX", block.get("index", 0))
+    s = ShardSettings(count=_as_int(count, "watcher.shard.count"), index=_as_int(index, "watcher.shard.index"),
+                      key=_choice(block.get("key", "namespace"), "watcher.shard.key", ("namespace", "uid")))
+    if s.count < 1 or not 0 <= s.index < s.count:
+        raise ConfigError(f"watcher.shard: index {s.index} outside [0, {s.count})")
+    return s
 
 
 def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
@@ -333,6 +355,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
             path=ck.get("path") or None,
             interval_seconds=_as_float(ck.get("interval_seconds", 5.0), "watcher.checkpoint.interval_seconds"),
         ),
+        shard=_shard(w.get("shard") or {}),
     )
 
     endpoints = c.get("endpoints") or {}
