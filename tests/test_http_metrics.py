@@ -1,0 +1,117 @@
+"""HTTP/1.1 response parser edge cases and the metrics endpoint."""
+
+import asyncio
+
+import pytest
+
+from conftest import run
+from k8s_watcher_amd.metrics import LatencyHistogram, Metrics, start_metrics_server
+from k8s_watcher_amd.net.http import HttpClient, HttpError, ResponseParser
+
+
+def parse_all(data, step=None, **reset):
+    p = ResponseParser()
+    p.reset(**reset)
+    done = []
+    p.on_complete = lambda q: done.append((q.status, q.headers, q.body()))
+    if step is None:
+        rest = p.feed(data)
+    else:
+        rest = b""
+        for i in range(0, len(data), step):
+            rest = p.feed(data[i:i + step])
+    return p, done, rest
+
+
+def test_content_length_and_keepalive():
+    p, done, rest = parse_all(b"HTTP/1.1 200 OK\r\nContent-Length: 5\r\nX-A: 1\r\n\r\nhelloEXTRA")
+    assert done[0][0] == 200 and done[0][2] == b"hello" and rest == b"EXTRA"
+    assert done[0][1]["x-a"] == "1" and p.keep_alive
+
+
+@pytest.mark.parametrize("step", [None, 1, 3, 7])
+def test_chunked_with_extensions_and_trailers(step):
+    data = (b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n"
+            b"5;ext=1\r\nhello\r\n6\r\n world\r\n0\r\nTrailer: x\r\n\r\n")
+    p, done, _ = parse_all(data, step)
+    assert done[0][2] == b"hello world"
+
+
+def test_connection_close_and_http10():
+    p, done, _ = parse_all(b"HTTP/1.1 200 OK\r\nConnection: close\r\nContent-Length: 0\r\n\r\n")
+    assert not p.keep_alive and done
+    p, done, _ = parse_all(b"HTTP/1.0 200 OK\r\nContent-Length: 0\r\n\r\n")
+    assert not p.keep_alive
+
+
+def test_until_close_body():
+    p, done, _ = parse_all(b"HTTP/1.1 200 OK\r\n\r\nabc")
+    assert not done
+    p.feed(b"def")
+    p.feed_eof()
+    assert done[0][2] == b"abcdef"
+
+
+def test_no_body_statuses_and_head():
+    _, done, rest = parse_all(b"HTTP/1.1 204 No Content\r\n\r\nHTTP/1.1")
+    assert done[0][0] == 204 and rest == b"HTTP/1.1"
+    _, done, _ = parse_all(b"HTTP/1.1 200 OK\r\nContent-Length: 10\r\n\r\n", no_body=True)
+    assert done[0][2] == b""
+
+
+def test_raw_chunked_passthrough():
+    got = []
+    p = ResponseParser()
+    p.reset(raw_chunked=True)
+    p.on_body = got.append
+    p.feed(b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n3\r\nabc\r\n")
+    p.feed(b"0\r\n\r\n")
+    assert b"".join(got) == b"3\r\nabc\r\n0\r\n\r\n" and p.state == ResponseParser.RAW
+
+
+def test_malformed_raises():
+    with pytest.raises(HttpError):
+        parse_all(b"NOTHTTP 200 OK\r\n\r\n")
+    with pytest.raises(HttpError):
+        parse_all(b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\nzz\r\n")
+    p = ResponseParser()
+    p.feed(b"HTTP/1.1 200 OK\r\nContent-Length: 10\r\n\r\nabc")
+    with pytest.raises(HttpError):
+        p.feed_eof()
+
+
+def test_latency_histogram_percentiles():
+    h = LatencyHistogram(record_samples=True)
+    for v in range(1, 101):
+        h.observe_ns(v * 1000)
+    assert h.percentile_ns(50) == 50_000 and h.percentile_ns(99) == 99_000
+    h2 = LatencyHistogram()
+    for v in range(1, 101):
+        h2.observe_ns(v * 1000)
+    assert 50_000 <= h2.percentile_ns(50) <= 60_000  # bucket upper bound
+
+
+def test_metrics_server_endpoints():
+    async def body():
+        m = Metrics()
+        m.inc("events_received", 7)
+        m.latency.observe_ns(2_000_000)
+        m.gauges["cached_pods"] = lambda: 3.0
+        srv = await start_metrics_server(m, "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        c = HttpClient(f"http://127.0.0.1:{port}")
+        metrics = (await c.request("GET", "/metrics")).text()
+        ready0 = (await c.request("GET", "/readyz")).status
+        m.ready = True
+        ready1 = (await c.request("GET", "/readyz")).status
+        health = (await c.request("GET", "/healthz")).status
+        missing = (await c.request("GET", "/nope")).status
+        await c.close()
+        srv.close()
+        return metrics, ready0, ready1, health, missing
+
+    metrics, r0, r1, h, nf = run(body())
+    assert "k8s_watcher_events_received_total 7" in metrics
+    assert "k8s_watcher_cached_pods 3.0" in metrics
+    assert 'k8s_watcher_notify_latency_seconds_bucket{le="+Inf"} 1' in metrics
+    assert (r0, r1, h, nf) == (503, 200, 200, 404)
