@@ -120,7 +120,7 @@ class WatcherService:
             return NullNotifier(self.metrics)
         log_events = w.log_events if w.log_events is not None else self.log.isEnabledFor(logging.INFO)
         return NotifierPool(c, self.metrics, ts_mode=w.event_timestamp, log_events=log_events,
-                            on_saturation=self._on_saturation)
+                            on_saturation=self._on_saturation, native=w.engine == "native")
 
     def _on_saturation(self, saturated: bool) -> None:
         for r in self.reflectors:

@@ -248,6 +248,56 @@ class ResponseParser:
             raise HttpError("connection closed mid-response")
 
 
+class PyResponseScanner:
+    """Python twin of ``_kwcore.ResponseScanner`` (same results, used without the extension).
+
+    ``feed(data)`` returns one item per complete response: the int status for
+    a 2xx keep-alive response, else ``(status, keep_alive, body)``.
+    """
+
+    def __init__(self) -> None:
+        self.parser = ResponseParser()
+        self._done: List[object] = []
+        self._arm()
+
+    def _arm(self) -> None:
+        self.parser.reset()
+        self.parser.on_complete = self._complete
+
+    def _complete(self, p: ResponseParser) -> None:
+        if 200 <= p.status < 300 and p.keep_alive:
+            self._done.append(p.status)
+        else:
+            self._done.append((p.status, p.keep_alive, p.body()))
+
+    def reset(self) -> None:
+        self._done = []
+        self._arm()
+
+    def feed(self, data: bytes) -> list:
+        try:
+            while data:
+                data = self.parser.feed(data)
+                if self.parser.state == ResponseParser.DONE:
+                    self._arm()
+        except HttpError as exc:
+            raise ValueError(str(exc)) from None
+        if self.parser.state == ResponseParser.UNTIL_CLOSE and self.parser.body_parts:
+            p = self.parser
+            self._done.append((p.status, False, p.body()))
+            self._arm()
+        out, self._done = self._done, []
+        return out
+
+
+def response_scanner(native: bool = True):
+    """``_kwcore.ResponseScanner`` when requested and built, else :class:`PyResponseScanner`."""
+    if native:
+        from ..ops.native import load
+        return load().ResponseScanner()
+    return PyResponseScanner()
+
+
 class _ClientProtocol(asyncio.Protocol):
     """One TCP/TLS connection; at most one outstanding request (no pipelining here)."""
 

@@ -1311,6 +1311,218 @@ PyMethodDef Decoder_methods[] = {
 
 PyTypeObject DecoderType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 
+// ----------------------------------------------------------------------------- ResponseScanner
+//
+// HTTP/1.1 response framing for the clusterapi notifier pool: one feed() per
+// socket read returns every complete response in it. A 2xx keep-alive
+// response is returned as its int status (no allocation); anything else as
+// (status, keep_alive, body) so the pool can log / close. Handles
+// Content-Length, chunked bodies, 1xx/204/304 and read-until-close framing.
+
+struct ScannerObject {
+    PyObject_HEAD
+    std::string* buf;
+    size_t pos;
+};
+
+bool ieq_prefix(const char* p, const char* e, const char* lit) {
+    size_t n = std::strlen(lit);
+    if ((size_t)(e - p) < n) return false;
+    for (size_t i = 0; i < n; ++i) {
+        char c = p[i];
+        if (c >= 'A' && c <= 'Z') c = (char)(c - 'A' + 'a');
+        if (c != lit[i]) return false;
+    }
+    return true;
+}
+
+bool contains_token_ci(const char* p, const char* e, const char* tok) {
+    size_t n = std::strlen(tok);
+    for (const char* q = p; q + n <= e; ++q)
+        if (ieq_prefix(q, e, tok)) return true;
+    return false;
+}
+
+// Try to parse one complete response at b[0..n). Returns bytes consumed (0 =
+// incomplete, SIZE_MAX = malformed); fills status, keep_alive, body span.
+size_t scan_response(const char* b, size_t n, int& status, bool& keep_alive, std::string& body,
+                     bool& until_close) {
+    const char* e = b + n;
+    const char* he = nullptr;
+    for (const char* q = b; q + 3 < e; ++q) {
+        q = (const char*)std::memchr(q, '\r', (size_t)(e - q));
+        if (!q || q + 3 >= e) break;
+        if (q[1] == '\n' && q[2] == '\r' && q[3] == '\n') {
+            he = q;
+            break;
+        }
+    }
+    if (!he) return n > 65536 ? SIZE_MAX : 0;
+    if (n < 12 || std::memcmp(b, "HTTP/1.", 7) != 0) return SIZE_MAX;
+    bool http10 = b[7] == '0';
+    const char* sp = (const char*)std::memchr(b, ' ', (size_t)(he - b));
+    if (!sp || he - sp < 4) return SIZE_MAX;
+    status = 0;
+    for (int i = 1; i <= 3; ++i) {
+        if (!is_digit(sp[i])) return SIZE_MAX;
+        status = status * 10 + (sp[i] - '0');
+    }
+    long long clen = -1;
+    bool chunked = false, conn_close = false, conn_keep = false;
+    const char* line = (const char*)std::memchr(b, '\n', (size_t)(he - b));
+    while (line && line < he) {
+        const char* ls = line + 1;
+        const char* le = (const char*)std::memchr(ls, '\r', (size_t)(he + 2 - ls));
+        if (!le) le = he;
+        if (ieq_prefix(ls, le, "content-length:")) {
+            const char* v = ls + 15;
+            while (v < le && (*v == ' ' || *v == '\t')) ++v;
+            clen = 0;
+            while (v < le && is_digit(*v)) clen = clen * 10 + (*v++ - '0');
+        } else if (ieq_prefix(ls, le, "transfer-encoding:")) {
+            chunked = contains_token_ci(ls + 18, le, "chunked");
+        } else if (ieq_prefix(ls, le, "connection:")) {
+            conn_close = contains_token_ci(ls + 11, le, "close");
+            conn_keep = contains_token_ci(ls + 11, le, "keep-alive");
+        }
+        line = (const char*)std::memchr(ls, '\n', (size_t)(he + 2 - ls));
+        if (line && line >= he) break;
+    }
+    keep_alive = http10 ? conn_keep : !conn_close;
+    const char* bs = he + 4;
+    body.clear();
+    until_close = false;
+    if ((status >= 100 && status < 200) || status == 204 || status == 304) return (size_t)(bs - b);
+    if (chunked) {
+        const char* q = bs;
+        while (true) {
+            const char* nl = (const char*)std::memchr(q, '\n', (size_t)(e - q));
+            if (!nl) return 0;
+            size_t sz = 0;
+            const char* h = q;
+            int digits = 0;
+            while (h < nl && hexval(*h) >= 0) {
+                sz = (sz << 4) | (size_t)hexval(*h++);
+                ++digits;
+            }
+            if (!digits) return SIZE_MAX;
+            q = nl + 1;
+            if (sz == 0) {
+                while (true) {  // trailers up to the empty line
+                    const char* t = (const char*)std::memchr(q, '\n', (size_t)(e - q));
+                    if (!t) return 0;
+                    bool empty = (t == q) || (t == q + 1 && *q == '\r');
+                    q = t + 1;
+                    if (empty) return (size_t)(q - b);
+                }
+            }
+            if ((size_t)(e - q) < sz + 2) return 0;
+            body.append(q, sz);
+            q += sz;
+            const char* crlf = (const char*)std::memchr(q, '\n', (size_t)(e - q));
+            if (!crlf) return 0;
+            q = crlf + 1;
+        }
+    }
+    if (clen >= 0) {
+        if ((size_t)(e - bs) < (size_t)clen) return 0;
+        body.assign(bs, (size_t)clen);
+        return (size_t)(bs - b) + (size_t)clen;
+    }
+    // no framing: body runs to EOF; report what is here and let the caller close
+    until_close = true;
+    keep_alive = false;
+    body.assign(bs, (size_t)(e - bs));
+    return n;
+}
+
+PyObject* Scanner_new(PyTypeObject* type, PyObject*, PyObject*) {
+    ScannerObject* self = (ScannerObject*)type->tp_alloc(type, 0);
+    if (!self) return nullptr;
+    self->buf = new std::string();
+    self->pos = 0;
+    return (PyObject*)self;
+}
+
+void Scanner_dealloc(ScannerObject* self) {
+    delete self->buf;
+    Py_TYPE(self)->tp_free((PyObject*)self);
+}
+
+PyObject* Scanner_feed(ScannerObject* self, PyObject* arg) {
+    Py_buffer view;
+    if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) < 0) return nullptr;
+    std::string& buf = *self->buf;
+    const char* data;
+    size_t n;
+    bool direct = buf.empty();
+    if (direct) {
+        data = (const char*)view.buf;
+        n = (size_t)view.len;
+    } else {
+        buf.append((const char*)view.buf, (size_t)view.len);
+        data = buf.data();
+        n = buf.size();
+    }
+    PyObject* out = PyList_New(0);
+    std::string body;
+    size_t pos = 0;
+    bool ok = out != nullptr;
+    while (ok && pos < n) {
+        int status = 0;
+        bool keep = true, until_close = false;
+        size_t used = scan_response(data + pos, n - pos, status, keep, body, until_close);
+        if (used == 0) break;
+        if (used == SIZE_MAX) {
+            PyErr_SetString(PyExc_ValueError, "malformed HTTP response");
+            ok = false;
+            break;
+        }
+        pos += used;
+        PyObject* item;
+        if (status >= 200 && status < 300 && keep) {
+            item = PyLong_FromLong(status);
+        } else {
+            item = Py_BuildValue("(iOy#)", status, keep ? Py_True : Py_False, body.data(),
+                                 (Py_ssize_t)body.size());
+        }
+        if (!item || PyList_Append(out, item) < 0) ok = false;
+        Py_XDECREF(item);
+        if (until_close) break;
+    }
+    if (ok) {
+        if (direct) {
+            if (pos < n) buf.assign(data + pos, n - pos);
+        } else {
+            buf.erase(0, pos);
+        }
+    }
+    PyBuffer_Release(&view);
+    if (!ok) {
+        Py_XDECREF(out);
+        return nullptr;
+    }
+    return out;
+}
+
+PyObject* Scanner_reset(ScannerObject* self, PyObject*) {
+    self->buf->clear();
+    Py_RETURN_NONE;
+}
+
+PyObject* Scanner_pending(ScannerObject* self, PyObject*) {
+    return PyLong_FromSize_t(self->buf->size());
+}
+
+PyMethodDef Scanner_methods[] = {
+    {"feed", (PyCFunction)Scanner_feed, METH_O,
+     "feed(bytes) -> [status | (status, keep_alive, body)] for each complete response"},
+    {"reset", (PyCFunction)Scanner_reset, METH_NOARGS, "drop buffered bytes"},
+    {"pending", (PyCFunction)Scanner_pending, METH_NOARGS, "buffered byte count"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyTypeObject ScannerType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
 // format_event_timestamp(utc: bool) -> str: datetime.now().isoformat() equivalent
 PyObject* kw_event_timestamp(PyObject*, PyObject* arg) {
     int utc = PyObject_IsTrue(arg);
@@ -1424,6 +1636,16 @@ PyMODINIT_FUNC PyInit__kwcore(void) {
     if (!m) return nullptr;
     Py_INCREF(&DecoderType);
     PyModule_AddObject(m, "StreamDecoder", (PyObject*)&DecoderType);
+    ScannerType.tp_name = "_kwcore.ResponseScanner";
+    ScannerType.tp_basicsize = sizeof(ScannerObject);
+    ScannerType.tp_flags = Py_TPFLAGS_DEFAULT;
+    ScannerType.tp_doc = "ResponseScanner(): incremental HTTP/1.1 response framing";
+    ScannerType.tp_methods = Scanner_methods;
+    ScannerType.tp_new = Scanner_new;
+    ScannerType.tp_dealloc = (destructor)Scanner_dealloc;
+    if (PyType_Ready(&ScannerType) < 0) return nullptr;
+    Py_INCREF(&ScannerType);
+    PyModule_AddObject(m, "ResponseScanner", (PyObject*)&ScannerType);
     const char* names[6] = {"ADDED", "MODIFIED", "DELETED", "BOOKMARK", "ERROR", "INVALID"};
     for (int i = 0; i < 6; ++i) {
         g_types[i] = PyUnicode_InternFromString(names[i]);

@@ -40,7 +40,7 @@ from urllib.parse import urlsplit
 
 from ..metrics import Metrics
 from ..models.payload import finish_body
-from ..net.http import ResponseParser
+from ..net.http import response_scanner
 from ..utils.backoff import Backoff
 from ..utils.config import ClusterApiSettings, RetryPolicy
 from ..utils.logsetup import NOTIFIER_LOGGER, SERVICE_LOGGER
@@ -77,36 +77,44 @@ class _Conn(asyncio.Protocol):
         self.transport: Optional[asyncio.Transport] = None
         self.queue: Deque[NotifyRequest] = collections.deque()
         self.inflight: Deque[NotifyRequest] = collections.deque()
-        self.parser = ResponseParser()
-        self._arm_parser()
+        self.scanner = response_scanner(pool.native)
         self.connect_backoff = Backoff(RetryPolicy(1_000_000, 0.05, 2.0, 5.0, 0.2))
         self.reconnect_handle: Optional[asyncio.TimerHandle] = None
-
-    def _arm_parser(self) -> None:
-        p = self.parser
-        p.reset()
-        p.on_complete = self._on_message
 
     # ------------------------------------------------------------- asyncio protocol
     def connection_made(self, transport) -> None:  # type: ignore[override]
         self.transport = transport
         self.state = self.UP
         self.connect_backoff.reset()
-        self._arm_parser()
+        self.scanner.reset()
         self.pump()
 
     def data_received(self, data: bytes) -> None:  # type: ignore[override]
-        parser = self.parser
         try:
-            while data:
-                data = parser.feed(data)
-                if parser.state == ResponseParser.DONE:
-                    self._arm_parser()
-        except Exception as exc:  # noqa: BLE001 - protocol violation: drop the connection
+            results = self.scanner.feed(data)
+        except ValueError as exc:  # protocol violation: drop the connection
             self.pool.log.error(f"Unexpected error calling clusterapi: {exc}")
             if self.transport is not None:
                 self.transport.abort()
             return
+        if results:
+            inflight = self.inflight
+            pool = self.pool
+            for r in results:
+                if not inflight:
+                    break  # unsolicited response; ignore
+                req = inflight.popleft()
+                if r.__class__ is int:
+                    pool._delivered(req)
+                    continue
+                status, keep_alive, body = r
+                if 200 <= status < 300:
+                    pool._delivered(req)
+                else:
+                    pool._failed(req, status, body[:500].decode("utf-8", "replace"))
+                if not keep_alive and self.transport is not None:
+                    self.transport.close()
+                    return
         self.pump()
 
     def connection_lost(self, exc) -> None:  # type: ignore[override]
@@ -121,18 +129,6 @@ class _Conn(asyncio.Protocol):
             self.schedule_connect()
 
     # ------------------------------------------------------------- internals
-    def _on_message(self, p: ResponseParser) -> None:
-        if not self.inflight:
-            return  # unsolicited response; ignore
-        req = self.inflight.popleft()
-        status = p.status
-        if 200 <= status < 300:
-            self.pool._delivered(req)
-        else:
-            self.pool._failed(req, status, p.body().decode("utf-8", "replace")[:500])
-        if not p.keep_alive and self.transport is not None:
-            self.transport.close()
-
     def schedule_connect(self) -> None:
         if self.state != self.IDLE or self.reconnect_handle is not None or self.pool.closing:
             return
@@ -201,8 +197,12 @@ class NotifierPool:
 
     def __init__(self, settings: ClusterApiSettings, metrics: Optional[Metrics] = None,
                  ts_mode: str = "local", log_events: bool = False, ssl_context=None,
-                 on_saturation: Optional[Callable[[bool], None]] = None) -> None:
+                 on_saturation: Optional[Callable[[bool], None]] = None, native: Optional[bool] = None) -> None:
         self.settings = settings
+        if native is None:
+            from ..ops.native import available
+            native = available()
+        self.native = native  # response framing in _kwcore.ResponseScanner
         self.metrics = metrics or Metrics()
         self.loop = asyncio.get_running_loop()
         self.log = logging.getLogger(NOTIFIER_LOGGER)
