@@ -115,7 +115,10 @@ class _Conn(asyncio.Protocol):
                 if not keep_alive and self.transport is not None:
                     self.transport.close()
                     return
-        self.pump()
+            # refill at the end of this loop tick: every response that arrived in
+            # the same epoll round frees its slot first, so one write() carries
+            # all the follow-up requests of this connection
+            pool._defer_pump(self)
 
     def connection_lost(self, exc) -> None:  # type: ignore[override]
         self.transport = None
@@ -243,6 +246,7 @@ class NotifierPool:
         self._idle_event = asyncio.Event()
         self._idle_event.set()
         self._dirty: List[_Conn] = []
+        self._flush_scheduled = False
         self.retry_policy = settings.retry
         self._watchdog = self.loop.create_task(self._watchdog_loop())
 
@@ -281,6 +285,16 @@ class NotifierPool:
         self._dirty = []
         for conn in dirty:
             conn.pump()
+
+    def _defer_pump(self, conn: "_Conn") -> None:
+        self._dirty.append(conn)
+        if not self._flush_scheduled:
+            self._flush_scheduled = True
+            self.loop.call_soon(self._deferred_flush)
+
+    def _deferred_flush(self) -> None:
+        self._flush_scheduled = False
+        self.flush()
 
     async def health_check(self, timeout: float = 5.0) -> bool:
         """``GET <health>``; True on 2xx (reference: ``clusterapi_client.py:55-61``)."""
