@@ -128,9 +128,12 @@ class RefEquivWatcher:
             self.notified += 1
             self.latencies_ns.append(time.monotonic_ns() - read_ns)
 
-    def run(self, api_url: str, n_events: int, on_connected=None) -> float:
+    def run(self, api_url: str, n_events: int, on_connected=None, warm_events: int = 0,
+            on_warm=None) -> float:
         """Watch until ``n_events`` pod events were handled; returns elapsed seconds
-        measured from ``on_connected()`` (which should trigger the replay)."""
+        measured from ``on_connected()`` (which should trigger the replay) or, with
+        ``warm_events``, from the moment that many events were handled (then
+        ``on_warm()`` is called)."""
         u = urlsplit(api_url)
         conn = http.client.HTTPConnection(u.hostname, u.port)
         conn.request("GET", "/api/v1/pods?watch=true")
@@ -139,6 +142,7 @@ class RefEquivWatcher:
         if on_connected is not None:
             on_connected()
             t0 = time.perf_counter()
+        warm = warm_events <= 0
         buf = b""
         while self.processed < n_events:
             chunk = resp.read1(65536)
@@ -155,6 +159,12 @@ class RefEquivWatcher:
                 obj = _Model(ev["object"])
                 self.handle_pod_event(ev["type"], obj, read_ns)
                 self.processed += 1
+                if not warm and self.processed >= warm_events:
+                    warm = True
+                    self.latencies_ns.clear()
+                    if on_warm is not None:
+                        on_warm()
+                    t0 = time.perf_counter()
         elapsed = time.perf_counter() - t0
         conn.close()
         return elapsed

@@ -1,22 +1,34 @@
 """High-rate watch replay server for benchmarks (the "mock API" of BASELINE.json).
 
 :class:`~.fake_apiserver.FakeApiServer` serialises every event as it happens,
-which caps it far below the watcher's speed. This server instead renders a
-churn *template* once (``pods_per_step`` pod lifecycles = 5 events each, see
-:func:`.podgen.churn_events`) and, per step, re-stamps it with fresh
-resourceVersions and pod uids — a byte splice, no JSON work — then streams it
-as one HTTP chunk per event, exactly like kube-apiserver, as fast as the
-client reads (``STEP``) or at a fixed rate (``PACE``).
+which caps it far below the watcher's speed. This server renders a *template*
+once and, per step, re-stamps it with fresh resourceVersions (and, for churn,
+fresh pod uids) by splicing bytes — no JSON work — then streams it as one HTTP
+chunk per event, like kube-apiserver, as fast as the client reads (``STEP``)
+or at a fixed rate (``PACE``).
+
+Templates (``--template``):
+
+* ``churn`` — ``--pods`` lifecycles per step: ADDED → 3×MODIFIED → DELETED
+  (BASELINE config #4, #5);
+* ``createdelete`` — ADDED → MODIFIED(Running) → DELETED (config #2);
+* ``steady`` — ``--pods`` pods exist from the start (served by LIST); each step
+  MODIFIES every pod once (config #3).
+
+It keeps enough state to behave like an API server across restarts: a
+LIST returns the live pods at the current resourceVersion; a watch with
+``resourceVersion=X`` first receives every event after ``X`` (re-rendered from
+the template); ``X`` older than the last compaction gets an ``ERROR`` 410 event.
 
 Control is line-based on stdin, replies on stdout::
 
     READY <port> <events_per_step>
-    STEP <k>                 -> SENT <k> <n>     (whole step, unthrottled)
-    PACE <k> <rate> <count>  -> SENT <k> <n>     (first <count> events at <rate>/s)
+    STEP <k> [drop=<n>] [expire=<n>]  -> SENT <k> <n>  whole step; optionally abort every
+                                          watch (drop) or compact + 410 them (expire) after n events
+    PACE <k> <rate> <count>           -> SENT <k> <n>  first <count> events at <rate>/s (rate 0 = max)
+    DROP | EXPIRE | BOOKMARK          -> SENT - <watchers>
+    WATCHERS                          -> SENT - <open watch streams>
     QUIT
-
-HTTP surface: ``/version``, ``/api/v1/namespaces``, an empty ``PodList`` for
-``/api/v1/pods``, and ``?watch=true`` streams that receive every step.
 """
 
 from __future__ import annotations
@@ -24,56 +36,146 @@ from __future__ import annotations
 import argparse
 import asyncio
 import json
+import re
 import sys
 import time
-from typing import List, Optional, Tuple
+from typing import Dict, List, Optional, Tuple
+from urllib.parse import parse_qs, urlsplit
 
-from .podgen import churn_events
+from .podgen import PodFactory, churn_events
 
 _HDR = (b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\n"
         b"Transfer-Encoding: chunked\r\n\r\n")
+_PH = re.compile(rb"@@(RV|UID|STEP)@@")
+RV0 = 10_000_000
+_TYPES = {"ADDED": b'{"type":"ADDED","object":', "MODIFIED": b'{"type":"MODIFIED","object":',
+          "DELETED": b'{"type":"DELETED","object":'}
+
+
+def _compile(obj: dict, uid: str) -> List:
+    raw = json.dumps(obj, separators=(",", ":"), ensure_ascii=False).encode("utf-8")
+    raw = raw.replace(uid.encode(), b"@@UID@@")
+    return _PH.split(raw)  # [lit, name, lit, name, ..., lit]
 
 
 class Template:
-    def __init__(self, pods_per_step: int, seed: int, namespaces: Optional[List[str]] = None) -> None:
-        # each event: (segments, uid-tail) where the line is
-        # seg0 + RV + seg1 + UID + seg2 + UID + ... and UID = <8-hex step tag> + uid-tail
-        self.events: List[Tuple[List[bytes], bytes]] = []
-        for etype, obj in churn_events(pods_per_step, seed=seed, namespaces=namespaces):
-            uid = obj["metadata"]["uid"].encode()
-            obj["metadata"]["resourceVersion"] = "@@RV@@"
-            line = json.dumps({"type": etype, "object": obj}, separators=(",", ":"),
-                              ensure_ascii=False).encode("utf-8") + b"\n"
-            pre, post = line.split(b"@@RV@@", 1)
-            segs = [pre] + post.split(uid)
-            self.events.append((segs, uid[8:]))
+    def __init__(self, kind: str, pods: int, seed: int = 0, namespaces: Optional[List[str]] = None) -> None:
+        self.kind = kind
+        self.events: List[Tuple[str, List, str]] = []   # (etype, segments, uid)
+        self.initial: List[Tuple[List, str]] = []       # steady: pods present before step 0
+        if kind == "churn":
+            for et, obj in churn_events(pods, seed=seed, namespaces=namespaces):
+                obj["metadata"]["resourceVersion"] = "@@RV@@"
+                uid = obj["metadata"]["uid"]
+                self.events.append((et, _compile(obj, uid), uid))
+        elif kind == "createdelete":
+            f = PodFactory(seed, namespaces)
+            for _ in range(pods):
+                p0 = f.new_pod()
+                p1 = f.running(p0)
+                p2 = f.deleting(p1)
+                for et, obj in (("ADDED", p0), ("MODIFIED", p1), ("DELETED", p2)):
+                    obj["metadata"]["resourceVersion"] = "@@RV@@"
+                    self.events.append((et, _compile(obj, p0["metadata"]["uid"]), p0["metadata"]["uid"]))
+        elif kind == "steady":
+            f = PodFactory(seed, namespaces)
+            for _ in range(pods):
+                p = f.running(f.new_pod())
+                p["metadata"]["resourceVersion"] = "@@RV@@"
+                p["metadata"]["annotations"]["k8s-watcher.test/generation"] = "@@STEP@@"
+                uid = p["metadata"]["uid"]
+                segs = _compile(p, uid)
+                self.initial.append((segs, uid))
+                self.events.append(("MODIFIED", segs, uid))
+        else:
+            raise ValueError(f"unknown template {kind!r}")
 
     def __len__(self) -> int:
         return len(self.events)
 
-    def render(self, step: int, start: int, stop: int, rv_base: int) -> bytes:
-        tag = b"%08x" % (step & 0xFFFFFFFF)
-        out = []
-        for i in range(start, stop):
-            segs, tail = self.events[i]
-            body = (tag + tail).join(segs[1:])
-            n = len(segs[0]) + len(body) + len(str(rv_base + i))
-            out.append(b"%x\r\n%s%d%s\r\n" % (n, segs[0], rv_base + i, body))
+    def uid(self, step: int, uid: str) -> str:
+        if self.kind == "steady":
+            return uid
+        return f"{step & 0xFFFFFFFF:08x}" + uid[8:]
+
+    def obj(self, segs: List, rv: int, uid: str, step: int) -> bytes:
+        sub = {b"RV": str(rv).encode(), b"UID": uid.encode(), b"STEP": str(step).encode()}
+        out = [segs[0]]
+        for j in range(1, len(segs), 2):
+            out.append(sub[segs[j]])
+            out.append(segs[j + 1])
         return b"".join(out)
+
+    def line(self, step: int, i: int) -> bytes:
+        et, segs, uid = self.events[i]
+        body = _TYPES[et] + self.obj(segs, RV0 + step * len(self) + i, self.uid(step, uid), step) + b"}\n"
+        return b"%x\r\n%s\r\n" % (len(body), body)
+
+    def render(self, step: int, start: int, stop: int) -> Tuple[bytes, List[int]]:
+        """Chunked bytes for events [start, stop) and each event's byte offset."""
+        parts, offsets, pos = [], [], 0
+        for i in range(start, stop):
+            b = self.line(step, i)
+            offsets.append(pos)
+            pos += len(b)
+            parts.append(b)
+        return b"".join(parts), offsets
 
 
 class ReplayServer:
     def __init__(self, template: Template, prerender: int = 0) -> None:
         self.t = template
+        self.E = len(template)
         self.watchers: List[asyncio.StreamWriter] = []
-        self.rv = 1000
+        self.rv = RV0 - 1 if template.kind != "steady" else RV0 - 1
+        self.compacted_rv = RV0 - 1
+        # live objects: uid -> (step, event index | -1 for the initial state)
+        self.live: Dict[str, Tuple[int, int]] = {}
+        if template.kind == "steady":
+            self.live = {uid: (-1, j) for j, (_, uid) in enumerate(template.initial)}
         # Whole steps rendered ahead of time so that, during a timed step, this
         # process only issues send() calls and can never be the bottleneck.
-        self.rendered = {k: self.t.render(k, 0, len(self.t), self.rv_base(k)) for k in range(prerender)}
+        self.rendered = {k: self.t.render(k, 0, self.E) for k in range(prerender)}
 
-    def rv_base(self, step: int) -> int:
-        return 10_000_000 + step * len(self.t)
+    # ------------------------------------------------------------------ state
+    def pos_of(self, rv: int) -> Tuple[int, int]:
+        return (rv - RV0) // self.E, (rv - RV0) % self.E
 
+    def _advance(self, step: int, start: int, stop: int) -> None:
+        t = self.t
+        for i in range(start, stop):
+            et, _, uid = t.events[i]
+            u = t.uid(step, uid)
+            if et == "DELETED":
+                self.live.pop(u, None)
+            else:
+                self.live[u] = (step, i)
+        self.rv = RV0 + step * self.E + stop - 1
+
+    def list_body(self) -> bytes:
+        items = []
+        t = self.t
+        for u, (step, i) in self.live.items():
+            if step < 0:
+                segs, _ = t.initial[i]
+                items.append(t.obj(segs, RV0 - 1, u, 0))
+            else:
+                _, segs, _ = t.events[i]
+                items.append(t.obj(segs, RV0 + step * self.E + i, u, step))
+        return (b'{"kind":"PodList","apiVersion":"v1","metadata":{"resourceVersion":"%d"},"items":[%s]}'
+                % (self.rv, b",".join(items)))
+
+    def backlog(self, since: int) -> bytes:
+        """Every event with resourceVersion in (since, self.rv]."""
+        out = []
+        rv = max(since, RV0 - 1) + 1
+        while rv <= self.rv:
+            step, i = self.pos_of(rv)
+            out.append(self.t.line(step, i))
+            rv += 1
+        return b"".join(out)
+
+    # ------------------------------------------------------------------ HTTP
     async def handle(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
         try:
             while True:
@@ -85,22 +187,21 @@ class ReplayServer:
                     if h in (b"\r\n", b"\n", b""):
                         break
                 target = line.split()[1].decode()
-                low = target.lower()
-                if "watch=true" in low or "watch=1" in low:
-                    writer.write(_HDR)
-                    self.watchers.append(writer)
+                u = urlsplit(target)
+                q = {k: v[-1] for k, v in parse_qs(u.query).items()}
+                if q.get("watch", "").lower() in ("true", "1"):
+                    self.start_watch(writer, q.get("resourceVersion"))
                     await reader.read()  # hold until the client goes away
                     return
-                if target.startswith("/version"):
+                if u.path == "/version":
                     body = b'{"major":"1","minor":"33","gitVersion":"v1.33.1-replay"}'
-                elif target.startswith("/api/v1/namespaces") and "/pods" not in target:
+                elif u.path == "/api/v1/namespaces":
                     body = json.dumps({"kind": "NamespaceList", "apiVersion": "v1", "metadata": {},
                                        "items": [{"metadata": {"name": "default"}}]}).encode()
                 else:
-                    body = json.dumps({"kind": "PodList", "apiVersion": "v1",
-                                       "metadata": {"resourceVersion": str(self.rv)}, "items": []}).encode()
-                writer.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n%s"
-                             % (len(body), body))
+                    body = self.list_body()
+                writer.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n"
+                             % len(body) + body)
                 await writer.drain()
         except (ConnectionError, asyncio.IncompleteReadError):
             return
@@ -109,39 +210,111 @@ class ReplayServer:
                 self.watchers.remove(writer)
             writer.close()
 
-    async def send(self, step: int, rate: Optional[float] = None, count: Optional[int] = None) -> int:
-        n = len(self.t) if count is None else min(count, len(self.t))
-        rv_base = self.rv_base(step)
+    def start_watch(self, writer: asyncio.StreamWriter, rv_param: Optional[str]) -> None:
+        """Synchronous: the backlog and the registration happen between two sends."""
+        writer.write(_HDR)
+        if rv_param not in (None, "", "0"):
+            since = int(rv_param)
+            if since < self.compacted_rv:
+                err = json.dumps({"type": "ERROR", "object": {
+                    "kind": "Status", "apiVersion": "v1", "status": "Failure", "reason": "Expired", "code": 410,
+                    "message": f"too old resource version: {since} ({self.compacted_rv})"}}).encode() + b"\n"
+                writer.write(b"%x\r\n%s\r\n0\r\n\r\n" % (len(err), err))
+                writer.close()
+                return
+            writer.write(self.backlog(since))
+        else:
+            # no resourceVersion: synthetic ADDED for every live pod, then live events
+            # (what kube-apiserver does, and what the reference's watch relies on)
+            t = self.t
+            for u, (step, i) in self.live.items():
+                if step < 0:
+                    segs, _ = t.initial[i]
+                    obj = t.obj(segs, RV0 - 1, u, 0)
+                else:
+                    obj = t.obj(t.events[i][1], RV0 + step * self.E + i, u, step)
+                body = _TYPES["ADDED"] + obj + b"}\n"
+                writer.write(b"%x\r\n%s\r\n" % (len(body), body))
+        self.watchers.append(writer)
+
+    def drop(self) -> int:
+        n = len(self.watchers)
+        for w in list(self.watchers):
+            w.transport.abort()
+        self.watchers.clear()
+        return n
+
+    def expire(self) -> int:
+        self.compacted_rv = self.rv
+        n = len(self.watchers)
+        err = json.dumps({"type": "ERROR", "object": {
+            "kind": "Status", "apiVersion": "v1", "status": "Failure", "reason": "Expired", "code": 410,
+            "message": "too old resource version"}}).encode() + b"\n"
+        for w in list(self.watchers):
+            w.write(b"%x\r\n%s\r\n0\r\n\r\n" % (len(err), err))
+            w.close()
+        self.watchers.clear()
+        return n
+
+    def bookmark(self) -> int:
+        line = (b'{"type":"BOOKMARK","object":{"kind":"Pod","apiVersion":"v1","metadata":'
+                b'{"resourceVersion":"%d"}}}\n' % self.rv)
+        for w in self.watchers:
+            w.write(b"%x\r\n%s\r\n" % (len(line), line))
+        return len(self.watchers)
+
+    # ------------------------------------------------------------------ streaming
+    async def _broadcast(self, data) -> None:
+        for w in list(self.watchers):
+            w.write(data)
+        for w in list(self.watchers):
+            try:
+                await w.drain()
+            except ConnectionError:
+                pass
+
+    async def send(self, step: int, rate: Optional[float] = None, count: Optional[int] = None,
+                   drop_at: Optional[int] = None, expire_at: Optional[int] = None) -> int:
+        n = self.E if count is None else min(count, self.E)
+        cut = drop_at if drop_at is not None else expire_at
         pre = self.rendered.pop(step, None)
-        if pre is not None and count is None:
-            view = memoryview(pre)
-            piece = 1 << 22
-            for a in range(0, len(view), piece):
-                for w in list(self.watchers):
-                    w.write(view[a:a + piece])
-                    await w.drain()
-        elif rate:
+        if rate:
             t0 = time.monotonic()
             for i in range(n):
-                data = self.t.render(step, i, i + 1, rv_base)
-                for w in list(self.watchers):
-                    w.write(data)
+                self._advance(step, i, i + 1)
+                await self._broadcast(self.t.line(step, i))
                 delay = t0 + (i + 1) / rate - time.monotonic()
                 if delay > 0:
                     await asyncio.sleep(delay)
+            return n
+        if pre is not None and count is None:
+            data, offsets = pre
         else:
-            slice_ = 256
-            for a in range(0, n, slice_):
-                data = self.t.render(step, a, min(n, a + slice_), rv_base)
-                for w in list(self.watchers):
-                    w.write(data)
-                    await w.drain()
-        self.rv = rv_base + n
+            data, offsets = self.t.render(step, 0, n)
+        offsets = offsets + [len(data)]
+        view = memoryview(data)
+        i = 0
+        while i < n:
+            j = min(n, i + 1024)
+            if cut is not None and i < cut <= j:
+                j = cut
+            # advance first: _broadcast writes before its first await, so a watch
+            # that joins while we wait for drains gets exactly the events after this slice
+            self._advance(step, i, j)
+            await self._broadcast(view[offsets[i]:offsets[j]])
+            i = j
+            if cut is not None and i == cut:
+                if drop_at is not None:
+                    self.drop()
+                else:
+                    self.expire()
+                cut = None
+                await asyncio.sleep(0)
         return n
 
 
 async def amain(args) -> None:
-    tmpl = Template(args.pods_per_step, args.seed, args.namespaces.split(",") if args.namespaces else None)
+    tmpl = Template(args.template, args.pods, args.seed, args.namespaces.split(",") if args.namespaces else None)
     srv = ReplayServer(tmpl, args.prerender)
     server = await asyncio.start_server(srv.handle, "127.0.0.1", args.port)
     port = server.sockets[0].getsockname()[1]
@@ -157,24 +330,34 @@ async def amain(args) -> None:
         if not parts:
             continue
         cmd = parts[0].upper()
+        opts = dict(p.split("=", 1) for p in parts[2:] if "=" in p)
         if cmd == "QUIT":
             break
         if cmd == "STEP":
-            n = await srv.send(int(parts[1]))
+            n = await srv.send(int(parts[1]), drop_at=int(opts["drop"]) if "drop" in opts else None,
+                               expire_at=int(opts["expire"]) if "expire" in opts else None)
         elif cmd == "PACE":
-            n = await srv.send(int(parts[1]), float(parts[2]), int(parts[3]))
+            rate = float(parts[2])
+            n = await srv.send(int(parts[1]), rate or None, int(parts[3]))
         elif cmd == "WATCHERS":
             n = sum(1 for w in srv.watchers if not w.is_closing())
+        elif cmd == "DROP":
+            n = srv.drop()
+        elif cmd == "EXPIRE":
+            n = srv.expire()
+        elif cmd == "BOOKMARK":
+            n = srv.bookmark()
         else:
             n = -1
-        print(f"SENT {parts[1] if len(parts) > 1 else '-'} {n}", flush=True)
+        print(f"SENT {parts[1] if len(parts) > 1 and cmd in ('STEP', 'PACE') else '-'} {n}", flush=True)
     server.close()
 
 
 def main(argv: Optional[List[str]] = None) -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--port", type=int, default=0)
-    ap.add_argument("--pods-per-step", type=int, default=10000)
+    ap.add_argument("--template", default="churn", choices=["churn", "createdelete", "steady"])
+    ap.add_argument("--pods", "--pods-per-step", dest="pods", type=int, default=10000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--namespaces", default=None)
     ap.add_argument("--prerender", type=int, default=0, help="render steps [0, N) before READY")

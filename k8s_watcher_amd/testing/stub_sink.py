@@ -62,6 +62,9 @@ class SinkState:
     def payloads(self) -> List[Dict]:
         return [json.loads(b) for _, b in self.received]
 
+    def note(self, body: bytes) -> None:
+        """Hook for every accepted payload (see ``_VerifyingState``)."""
+
     def _notify_waiters(self) -> None:
         if not self.waiters:
             return
@@ -133,6 +136,7 @@ class _SinkProtocol(asyncio.Protocol):
                 responses.append(_resp(fail, b'{"error":"injected"}'))
                 continue
             st.count += 1
+            st.note(body)
             if st.record:
                 st.received.append((now, body))
                 st.heads.append(head)
@@ -196,8 +200,40 @@ class StubSink:
                 pass
 
 
-def run_sink_process(port: int, workers: int = 1, latency: float = 0.0) -> None:
-    """Blocking: serve on ``port`` with ``workers`` SO_REUSEPORT processes (bench helper)."""
+def payload_key(body: bytes) -> bytes:
+    """``uid|event_type|phase`` of a payload without a JSON parse (soak verification).
+
+    The first ``"uid":`` in a payload is the top-level one (``name`` and
+    ``namespace`` precede it and are plain strings)."""
+    i = body.find(b'"uid":"') + 7
+    uid = body[i:body.find(b'"', i)]
+    j = body.rfind(b'"event_type":"') + 14
+    et = body[j:body.find(b'"', j)]
+    k = body.find(b'"status":{"phase":') + 18
+    phase = body[k:body.find(b",", k)].strip(b'"')
+    return b"|".join((uid, et, phase))
+
+
+class _VerifyingState(SinkState):
+    """Counts every payload key; dumped as JSON when the worker is told to stop."""
+
+    def __init__(self, **kw) -> None:
+        super().__init__(record=False, **kw)
+        self.keys: Dict[bytes, int] = {}
+
+    def note(self, body: bytes) -> None:
+        k = payload_key(body)
+        self.keys[k] = self.keys.get(k, 0) + 1
+
+
+def run_sink_process(port: int, workers: int = 1, latency: float = 0.0,
+                     verify_dir: Optional[str] = None) -> None:
+    """Blocking: serve on ``port`` with ``workers`` SO_REUSEPORT processes (bench helper).
+
+    With ``verify_dir`` every worker records ``uid|event_type|phase`` counts and
+    writes them to ``verify_dir/sink-<pid>.json`` on SIGTERM.
+    """
+    import signal as _signal
     pids = []
     for _ in range(workers - 1):
         pid = os.fork()
@@ -208,8 +244,17 @@ def run_sink_process(port: int, workers: int = 1, latency: float = 0.0) -> None:
 
     async def serve() -> None:
         sink = StubSink(record=False, latency=latency)
+        if verify_dir:
+            sink.state = _VerifyingState(latency=latency)
         await sink.start("127.0.0.1", port, reuse_port=True)
-        await asyncio.Event().wait()
+        stop = asyncio.Event()
+        loop = asyncio.get_running_loop()
+        loop.add_signal_handler(_signal.SIGTERM, stop.set)
+        await stop.wait()
+        if verify_dir:
+            st = sink.state
+            with open(os.path.join(verify_dir, f"sink-{os.getpid()}.json"), "w") as fh:
+                json.dump({"count": st.count, "keys": {k.decode(): v for k, v in st.keys.items()}}, fh)
 
     try:
         asyncio.run(serve())
@@ -222,9 +267,10 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--port", type=int, default=3000)
     ap.add_argument("--workers", type=int, default=1)
     ap.add_argument("--latency", type=float, default=0.0)
+    ap.add_argument("--verify-dir", default=None, help="record payload keys, dump on SIGTERM")
     args = ap.parse_args(argv)
     print(f"stub clusterapi listening on http://127.0.0.1:{args.port}", flush=True)
-    run_sink_process(args.port, args.workers, args.latency)
+    run_sink_process(args.port, args.workers, args.latency, args.verify_dir)
 
 
 if __name__ == "__main__":
