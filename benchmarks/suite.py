@@ -223,14 +223,19 @@ async def run_reference(srv: Servers, profile: str, namespaces: List[str], criti
     if pace:
         ref2 = RefEquivWatcher(profile, namespaces, critical, f"http://127.0.0.1:{srv.sink_port}")
         connected2 = loop.create_future()
+        warmed2 = loop.create_future()
         n = int(pace.split()[3])
         th2 = threading.Thread(target=lambda: ref2.run(
-            f"http://127.0.0.1:{srv.api_port}", n,
-            on_connected=lambda: loop.call_soon_threadsafe(connected2.set_result, None)), daemon=True)
+            f"http://127.0.0.1:{srv.api_port}", warm + n,
+            on_connected=lambda: loop.call_soon_threadsafe(connected2.set_result, None),
+            warm_events=warm, on_warm=lambda: loop.call_soon_threadsafe(warmed2.set_result, None)),
+            daemon=True)
         await srv.wait_watchers(0)
         th2.start()
         await connected2
         await srv.wait_watchers(1)
+        if warm:
+            await warmed2
         await srv.cmd(pace)
         while th2.is_alive():
             await asyncio.sleep(0.01)
@@ -258,7 +263,7 @@ async def config2(a) -> dict:
         ours = await run_ours(srv, "development", {}, [f"STEP {k}" for k in range(1, steps + 1)],
                               ["STEP 0"], f"PACE {steps + 1} 100 {min(e, 200)}")
         ref = await run_reference(srv, "development", ["default", "kube-system"], False, e, 0,
-                                  f"STEP {steps + 2}", None)
+                                  f"STEP {steps + 2}", f"PACE {steps + 3} 100 {min(e, 200)}")
     return {"ours": ours, "reference_equiv": ref}
 
 
@@ -269,7 +274,7 @@ async def config3(a) -> dict:
         ours = await run_ours(srv, "staging", ov, [f"STEP {k}" for k in range(1, steps + 1)], ["STEP 0"],
                               f"PACE {steps + 1} 10 {max(10, int(30 * a.scale))}")
         ref = await run_reference(srv, "staging", ["default"], False, 1000, 1000, f"STEP {steps + 2}",
-                                  None)
+                                  f"PACE {steps + 3} 10 {max(10, int(30 * a.scale))}")
     return {"ours": ours, "reference_equiv": ref}
 
 
@@ -362,7 +367,8 @@ def main(argv=None) -> int:
     results = {}
     for k in [int(x) for x in a.only.split(",") if x]:
         profile = {1: "development", 2: "development", 3: "staging", 4: "production", 5: "staging"}[k]
-        level = load_settings(profile).watcher.log_level
+        # config 5 is a soak of the resume machinery: per-event INFO lines are off there
+        level = "WARNING" if k == 5 else load_settings(profile).watcher.log_level
         setup_logging(profile, level, log_file=log_path)
         logging.getLogger("watcher.pod_watcher").setLevel(logging.NOTSET)
         t = time.time()

@@ -27,6 +27,7 @@ from ..ops.decode import (ADDED, BOOKMARK, DELETED, E_EXTRA, E_HAS_STATUS, E_NAM
 from ..ops.filters import TERMINAL_PHASES
 from ..parallel.shard import ShardFilter
 from ..utils.config import Settings
+from ..utils.fastlog import EventLog
 from ..utils.logsetup import SERVICE_LOGGER
 from ..utils.timefmt import event_timestamp
 
@@ -35,7 +36,7 @@ _POD_EVENTS = frozenset({ADDED, MODIFIED, DELETED})
 
 class EventPipeline:
     def __init__(self, settings: Settings, decoder, notifier, metrics: Metrics,
-                 cache: Optional[PodCache] = None) -> None:
+                 cache: Optional[PodCache] = None, event_log: Optional[EventLog] = None) -> None:
         w = settings.watcher
         self.settings = settings
         self.decoder = decoder
@@ -43,6 +44,7 @@ class EventPipeline:
         self.metrics = metrics
         self.cache = cache if cache is not None else PodCache()
         self.log = logging.getLogger(SERVICE_LOGGER)
+        self.elog = event_log if event_log is not None else EventLog(self.log)
         self.critical_active = settings.environment == "production" and w.critical_events_only
         self.namespaces = frozenset(w.namespaces)
         self.phase_mode = w.notify_on == "phase_change"
@@ -65,9 +67,9 @@ class EventPipeline:
         critical = self.critical_active
         nsset = self.namespaces
         phase_mode = self.phase_mode
-        log = self.log
+        elog = self.elog
         log_events = self.log_events
-        log_debug = log_events and log.isEnabledFor(logging.DEBUG)
+        log_debug = log_events and elog.enabled(logging.DEBUG)
         decoder = self.decoder
         submit = self.notifier.submit
         shard = self.shard if self.shard.active else None
@@ -111,10 +113,10 @@ class EventPipeline:
                 c["events_filtered_critical"] += 1
                 continue
             if log_events:
-                log.info("Pod event detected: %s - %s/%s", et, ns, name)
+                elog.log(logging.INFO, f"Pod event detected: {et} - {ns}/{name}")
             if nsset and ns not in nsset:
                 if log_debug:
-                    log.debug("Skipping pod %s/%s - not in target namespaces", ns, name)
+                    elog.log(logging.DEBUG, f"Skipping pod {ns}/{name} - not in target namespaces")
                 c["events_filtered_namespace"] += 1
                 continue
             if phase_mode and not (et == DELETED or prev is MISSING or prev != phase):
@@ -129,6 +131,7 @@ class EventPipeline:
                 ts = event_timestamp(self.ts_mode)
             submit(uid, et, ns, name, core, read_ns, ts)
         self.notifier.flush()
+        elog.flush()
         return ctrl
 
     # ------------------------------------------------------------------ relist

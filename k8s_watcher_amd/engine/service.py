@@ -37,6 +37,7 @@ from ..ops.decode import make_decoder
 from ..parallel.notifier import NotifierPool, NullNotifier
 from ..parallel.shard import ShardFilter
 from ..utils.config import Settings
+from ..utils.fastlog import EventLog
 from ..utils.logsetup import SERVICE_LOGGER
 from .checkpoint import load_checkpoint, save_checkpoint
 from .pipeline import EventPipeline
@@ -120,7 +121,8 @@ class WatcherService:
             return NullNotifier(self.metrics)
         log_events = w.log_events if w.log_events is not None else self.log.isEnabledFor(logging.INFO)
         return NotifierPool(c, self.metrics, ts_mode=w.event_timestamp, log_events=log_events,
-                            on_saturation=self._on_saturation, native=w.engine == "native")
+                            on_saturation=self._on_saturation, native=w.engine == "native",
+                            event_log=self.event_log)
 
     def _on_saturation(self, saturated: bool) -> None:
         for r in self.reflectors:
@@ -134,12 +136,15 @@ class WatcherService:
             self.log.error("Failed to setup Kubernetes client")
             raise SetupError("Failed to setup Kubernetes client")
         assert self.api is not None
+        self.event_log = EventLog(self.log)  # after logging is configured: picks the fast path
         self.notifier = self._make_notifier()
         if s.clusterapi.enabled and s.clusterapi.health_check_on_start:
             if await self.notifier.health_check():
                 self.log.info("ClusterAPI health check passed")
             else:
                 self.log.warning("ClusterAPI health check failed, but continuing...")
+        if s.clusterapi.enabled and hasattr(self.notifier, "warm_up"):
+            await self.notifier.warm_up()
         self.decoder = make_decoder(s.watcher.engine, s.environment, s.watcher.state_format)
         scopes = (ShardFilter(s.watcher.shard).namespaces(s.watcher.namespaces)
                   if s.watcher.namespace_scope == "server" and s.watcher.namespaces else [None])
@@ -154,7 +159,7 @@ class WatcherService:
             if loaded is not None:
                 saved_rvs, cache, _ = loaded
                 self.log.info(f"Resuming from checkpoint {ck}: {len(cache)} cached pods")
-        self.pipeline = EventPipeline(s, self.decoder, self.notifier, self.metrics, cache)
+        self.pipeline = EventPipeline(s, self.decoder, self.notifier, self.metrics, cache, self.event_log)
         self.metrics.gauges["cached_pods"] = lambda: float(len(cache))
         self.metrics.gauges["notify_outstanding"] = lambda: float(self.notifier.outstanding())
         self.log.info(f"Starting Pod watcher in {s.environment} environment...")
@@ -183,7 +188,8 @@ class WatcherService:
 
     def _scope_pipeline(self, decoder) -> EventPipeline:
         assert self.pipeline is not None
-        p = EventPipeline(self.settings, decoder, self.notifier, self.metrics, self.pipeline.cache)
+        p = EventPipeline(self.settings, decoder, self.notifier, self.metrics, self.pipeline.cache,
+                          self.event_log)
         return p
 
     async def _wait_synced(self) -> None:

@@ -43,6 +43,7 @@ from ..models.payload import finish_body
 from ..net.http import response_scanner
 from ..utils.backoff import Backoff
 from ..utils.config import ClusterApiSettings, RetryPolicy
+from ..utils.fastlog import EventLog
 from ..utils.logsetup import NOTIFIER_LOGGER, SERVICE_LOGGER
 from ..utils.aio import with_timeout
 
@@ -114,7 +115,9 @@ class _Conn(asyncio.Protocol):
                     pool._failed(req, status, body[:500].decode("utf-8", "replace"))
                 if not keep_alive and self.transport is not None:
                     self.transport.close()
+                    pool.elog.flush()
                     return
+            pool.elog.flush()
             # refill at the end of this loop tick: every response that arrived in
             # the same epoll round frees its slot first, so one write() carries
             # all the follow-up requests of this connection
@@ -200,7 +203,8 @@ class NotifierPool:
 
     def __init__(self, settings: ClusterApiSettings, metrics: Optional[Metrics] = None,
                  ts_mode: str = "local", log_events: bool = False, ssl_context=None,
-                 on_saturation: Optional[Callable[[bool], None]] = None, native: Optional[bool] = None) -> None:
+                 on_saturation: Optional[Callable[[bool], None]] = None, native: Optional[bool] = None,
+                 event_log: Optional[EventLog] = None) -> None:
         self.settings = settings
         if native is None:
             from ..ops.native import available
@@ -210,6 +214,7 @@ class NotifierPool:
         self.loop = asyncio.get_running_loop()
         self.log = logging.getLogger(NOTIFIER_LOGGER)
         self.svc_log = logging.getLogger(SERVICE_LOGGER)
+        self.elog = event_log if event_log is not None else EventLog(self.svc_log)
         self.log_events = log_events
         self.ts_mode = ts_mode
         u = urlsplit(settings.base_url)
@@ -308,6 +313,22 @@ class NotifierPool:
         finally:
             await client.close()
 
+    async def warm_up(self, timeout: float = 2.0) -> int:
+        """Open every pooled connection now, so the first events do not pay for TCP/TLS setup.
+
+        Returns the number of connections up; failures are not errors (the
+        pool reconnects on demand).
+        """
+        for c in self.conns:
+            if c.state == _Conn.IDLE:
+                c.schedule_connect()
+        deadline = self.loop.time() + timeout
+        while self.loop.time() < deadline and any(c.state != _Conn.UP for c in self.conns):
+            if all(c.state == _Conn.IDLE and c.reconnect_handle is None for c in self.conns):
+                break  # every attempt failed; do not wait out the timeout
+            await asyncio.sleep(0.005)
+        return sum(c.state == _Conn.UP for c in self.conns)
+
     async def drain(self, timeout: Optional[float] = None) -> bool:
         self.flush()
         try:
@@ -352,7 +373,8 @@ class NotifierPool:
         if self.latest.get(req.uid) == req.seq:
             del self.latest[req.uid]
         if self.log_events:
-            self.svc_log.info(f"Successfully notified clusterapi about {req.etype} event for {req.ns}/{req.name}")
+            self.elog.log(logging.INFO,
+                          f"Successfully notified clusterapi about {req.etype} event for {req.ns}/{req.name}")
         self._add_pending(-1)
 
     def _failed(self, req: NotifyRequest, status: Optional[int], detail: str) -> None:
