@@ -34,6 +34,7 @@ from ..metrics import Metrics, start_metrics_server
 from ..net.http import HttpError
 from ..ops.cache import PodCache
 from ..ops.decode import make_decoder
+from ..parallel.native_notifier import NativeNotifierPool
 from ..parallel.notifier import NotifierPool, NullNotifier
 from ..parallel.shard import ShardFilter
 from ..utils.config import Settings
@@ -120,6 +121,10 @@ class WatcherService:
         if not c.enabled:
             return NullNotifier(self.metrics)
         log_events = w.log_events if w.log_events is not None else self.log.isEnabledFor(logging.INFO)
+        if w.engine == "native" and c.base_url.startswith("http://"):
+            # per-request work in C++ (ops/csrc/engine.inc); TLS endpoints use the asyncio pool
+            return NativeNotifierPool(c, self.metrics, ts_mode=w.event_timestamp, log_events=log_events,
+                                      on_saturation=self._on_saturation, event_log=self.event_log)
         return NotifierPool(c, self.metrics, ts_mode=w.event_timestamp, log_events=log_events,
                             on_saturation=self._on_saturation, native=w.engine == "native",
                             event_log=self.event_log)

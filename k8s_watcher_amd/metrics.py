@@ -58,6 +58,17 @@ class LatencyHistogram:
         if self.samples is not None:
             self.samples.append(ns)
 
+    def observe_many(self, values: "array.array") -> None:
+        """Bulk observe (int64 nanoseconds), e.g. latencies reported by the native notifier."""
+        counts = self.counts
+        bl = bisect.bisect_left
+        for ns in values:
+            counts[bl(_BUCKETS_NS, ns)] += 1
+        self.total_ns += sum(values)
+        self.n += len(values)
+        if self.samples is not None:
+            self.samples.extend(values)
+
     def reset(self) -> None:
         self.counts = [0] * (len(_BUCKETS_NS) + 1)
         self.total_ns = 0

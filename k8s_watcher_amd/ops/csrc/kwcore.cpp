@@ -18,8 +18,17 @@
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 
+#include <sys/socket.h>
+#include <sys/types.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <ctime>
+#include <deque>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -1611,6 +1620,8 @@ PyObject* kw_bench_parse(PyObject*, PyObject* args) {
     return Py_BuildValue("(dn)", secs, (Py_ssize_t)sink);
 }
 
+#include "engine.inc"
+
 PyMethodDef module_methods[] = {
     {"bench_parse", (PyCFunction)kw_bench_parse, METH_VARARGS, "bench_parse(data, mode=2, repeat=1)"},
     {"event_timestamp", (PyCFunction)kw_event_timestamp, METH_O, "event_timestamp(utc) -> str"},
@@ -1646,6 +1657,7 @@ PyMODINIT_FUNC PyInit__kwcore(void) {
     if (PyType_Ready(&ScannerType) < 0) return nullptr;
     Py_INCREF(&ScannerType);
     PyModule_AddObject(m, "ResponseScanner", (PyObject*)&ScannerType);
+    if (register_engine(m) < 0) return nullptr;
     const char* names[6] = {"ADDED", "MODIFIED", "DELETED", "BOOKMARK", "ERROR", "INVALID"};
     for (int i = 0; i < 6; ++i) {
         g_types[i] = PyUnicode_InternFromString(names[i]);

@@ -36,12 +36,17 @@ def compiler() -> str:
 def build_command() -> list:
     inc = sysconfig.get_paths()["include"]
     return [compiler(), "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
-            "-fno-strict-aliasing", "-Wall", "-Wno-shadow", "-Wno-unused-function",
-            f"-I{inc}", SRC, "-o", SO]
+            "-fno-strict-aliasing", "-Wall", "-Wno-shadow", "-Wno-unused-function", "-Wno-psabi",
+            f"-I{inc}", f"-I{os.path.dirname(SRC)}", SRC, "-o", SO]
+
+
+def sources() -> list:
+    d = os.path.dirname(SRC)
+    return [os.path.join(d, f) for f in sorted(os.listdir(d)) if f.endswith((".cpp", ".inc", ".h"))]
 
 
 def is_fresh() -> bool:
-    return os.path.exists(SO) and os.path.getmtime(SO) >= os.path.getmtime(SRC)
+    return os.path.exists(SO) and all(os.path.getmtime(SO) >= os.path.getmtime(s) for s in sources())
 
 
 def build(quiet: bool = False) -> str:

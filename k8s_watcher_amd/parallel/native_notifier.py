@@ -1,0 +1,251 @@
+"""clusterapi notifier pool on the native core (``_kwcore.Notifier``).
+
+Same contract and semantics as :class:`.notifier.NotifierPool` — per-pod
+ordering on a ``crc32(uid)``-chosen connection, pipelined keep-alive
+requests, any-2xx success, retries only while still the pod's newest
+notification (else *superseded*), optional coalescing, per-request timeout,
+backpressure — with the per-request work moved to C++ (``ops/csrc/engine.inc``):
+request framing, the send buffers, ``send``/``recv`` on non-blocking sockets,
+HTTP response framing, the in-flight windows and the retry decisions.
+
+This wrapper owns the asyncio side only: it connects sockets
+(``loop.sock_connect``) and hands their fds to the core, registers
+``add_reader``/``add_writer`` callbacks that call straight into C++, turns
+the core's retry decisions into ``call_later`` timers, writes the log lines
+the core reports and feeds its latency samples into :class:`Metrics`.
+
+Plain HTTP only: for an ``https`` clusterapi the service uses the asyncio
+pool, whose transports do TLS.
+"""
+
+from __future__ import annotations
+
+import array
+import asyncio
+import logging
+import socket
+from typing import Callable, Dict, Optional
+from urllib.parse import urlsplit
+
+from ..metrics import Metrics
+from ..net.http import HttpClient
+from ..ops.native import load
+from ..utils.aio import with_timeout
+from ..utils.backoff import Backoff
+from ..utils.config import ClusterApiSettings, RetryPolicy
+from ..utils.fastlog import EventLog
+from ..utils.logsetup import NOTIFIER_LOGGER, SERVICE_LOGGER
+from .notifier import RETRYABLE_STATUS
+
+
+class NativeNotifierPool:
+    def __init__(self, settings: ClusterApiSettings, metrics: Optional[Metrics] = None,
+                 ts_mode: str = "local", log_events: bool = False,
+                 on_saturation: Optional[Callable[[bool], None]] = None,
+                 event_log: Optional[EventLog] = None, **_ignored) -> None:
+        u = urlsplit(settings.base_url)
+        if u.scheme != "http":
+            raise ValueError("NativeNotifierPool supports plain http clusterapi URLs only")
+        self.settings = settings
+        self.metrics = metrics or Metrics()
+        self.loop = asyncio.get_running_loop()
+        self.log = logging.getLogger(NOTIFIER_LOGGER)
+        self.svc_log = logging.getLogger(SERVICE_LOGGER)
+        self.elog = event_log if event_log is not None else EventLog(self.svc_log)
+        self.log_events = log_events
+        self.host = u.hostname or "localhost"
+        self.port = u.port or 80
+        self.endpoint_url = settings.base_url + settings.pod_update
+        path = (u.path.rstrip("/") + settings.pod_update) or "/"
+        host_hdr = self.host if self.port == 80 else f"{self.host}:{self.port}"
+        head = (f"POST {path} HTTP/1.1\r\nHost: {host_hdr}\r\nContent-Type: application/json\r\n"
+                f"User-Agent: k8s-watcher-amd/1.0\r\n")
+        if settings.api_key:
+            head += f"Authorization: Bearer {settings.api_key}\r\n"
+        head += "Content-Length: "
+        r = settings.retry
+        self.core = load().Notifier(
+            head.encode("latin-1"), settings.pool.connections, settings.pool.pipeline_depth, r.max_attempts,
+            r.delay_seconds, r.multiplier, r.max_delay_seconds, settings.pool.coalesce, log_events,
+            sorted(RETRYABLE_STATUS), self.metrics.c)
+        self.n = settings.pool.connections
+        self.socks: Dict[int, socket.socket] = {}
+        self.connecting: set = set()
+        self.writers: set = set()
+        self.backoff = [Backoff(RetryPolicy(1_000_000, 0.05, 2.0, 5.0, 0.2)) for _ in range(self.n)]
+        self.reconnect: Dict[int, asyncio.TimerHandle] = {}
+        self.addr = None
+        self.high_water = settings.pool.queue_size
+        self.low_water = max(1, settings.pool.queue_size // 2)
+        self.saturated = False
+        self.on_saturation = on_saturation
+        self.closing = False
+        self._watchdog = self.loop.create_task(self._watchdog_loop())
+
+    # ------------------------------------------------------------------ API (NotifierPool-compatible)
+    def submit(self, uid, etype, ns, name, core: bytes, read_ns: int, ts: str) -> None:
+        self.core.submit(uid, etype, ns, name, core, ts, read_ns)
+
+    def flush(self) -> None:
+        self.core.flush()
+        self._after()
+
+    def outstanding(self) -> int:
+        return self.core.pending()
+
+    async def health_check(self, timeout: float = 5.0) -> bool:
+        client = HttpClient(self.settings.base_url, timeout=timeout)
+        try:
+            return (await client.request("GET", self.settings.health)).ok
+        except Exception:  # noqa: BLE001 - parity: any failure -> False
+            return False
+        finally:
+            await client.close()
+
+    async def warm_up(self, timeout: float = 2.0) -> int:
+        await asyncio.gather(*[self._connect(i) for i in range(self.n) if i not in self.socks],
+                             return_exceptions=True)
+        return len(self.socks)
+
+    async def drain(self, timeout: Optional[float] = None) -> bool:
+        self.flush()
+        deadline = None if timeout is None else self.loop.time() + timeout
+        while self.core.pending() > 0:
+            if deadline is not None and self.loop.time() > deadline:
+                return False
+            await asyncio.sleep(0.001)
+        return True
+
+    async def close(self) -> None:
+        self.closing = True
+        self._watchdog.cancel()
+        for h in self.reconnect.values():
+            h.cancel()
+        for i in list(self.socks):
+            self._drop_socket(i)
+            self.core.detach(i, "closing")
+        self.core.give_up_all()
+        self._after()
+        await asyncio.sleep(0)
+
+    # ------------------------------------------------------------------ sockets
+    async def _resolve(self):
+        if self.addr is None:
+            infos = await self.loop.getaddrinfo(self.host, self.port, type=socket.SOCK_STREAM)
+            self.addr = infos[0]
+        return self.addr
+
+    async def _connect(self, i: int) -> None:
+        if i in self.socks or i in self.connecting or self.closing:
+            return
+        self.connecting.add(i)
+        sock = None
+        try:
+            family, stype, proto, _, sa = await self._resolve()
+            sock = socket.socket(family, stype, proto)
+            sock.setblocking(False)
+            sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            await with_timeout(self.loop.sock_connect(sock, sa), self.settings.timeout)
+        except (OSError, asyncio.TimeoutError) as exc:
+            if sock is not None:
+                sock.close()
+            self.connecting.discard(i)
+            self.core.connect_failed(i, f"Connection error: Unable to connect to clusterapi at "
+                                        f"{self.endpoint_url} ({exc.__class__.__name__})")
+            self._after(connect_failed=i)
+            return
+        self.connecting.discard(i)
+        if self.closing:
+            sock.close()
+            return
+        self.socks[i] = sock
+        self.backoff[i].reset()
+        self.core.attach(i, sock.fileno())
+        self.loop.add_reader(sock.fileno(), self._readable, i)
+        self.core.flush()
+        self._after()
+
+    def _schedule_connect(self, i: int, failed: bool = False) -> None:
+        if i in self.socks or i in self.connecting or i in self.reconnect or self.closing:
+            return
+        delay = self.backoff[i].next_delay() if failed else 0.0
+
+        def fire() -> None:
+            self.reconnect.pop(i, None)
+            self.loop.create_task(self._connect(i))
+
+        self.reconnect[i] = self.loop.call_later(delay, fire)
+
+    def _drop_socket(self, i: int) -> None:
+        sock = self.socks.pop(i, None)
+        if sock is None:
+            return
+        fd = sock.fileno()
+        self.loop.remove_reader(fd)
+        if i in self.writers:
+            self.loop.remove_writer(fd)
+            self.writers.discard(i)
+        sock.close()
+
+    # ------------------------------------------------------------------ loop callbacks
+    def _readable(self, i: int) -> None:
+        self.core.on_readable(i)
+        self._after()
+
+    def _writable(self, i: int) -> None:
+        if not self.core.on_writable(i):
+            sock = self.socks.get(i)
+            if sock is not None:
+                self.loop.remove_writer(sock.fileno())
+            self.writers.discard(i)
+        self._after()
+
+    def _requeue(self, seq: int) -> None:
+        self.core.requeue(seq, self.closing)
+        self._after()
+
+    def _after(self, connect_failed: Optional[int] = None) -> None:
+        retries, logs, need_connect, want_write, lost, lat = self.core.take()
+        for i in lost:
+            self._drop_socket(i)
+        for seq, delay in retries:
+            self.loop.call_later(delay, self._requeue, seq)
+        if logs:
+            elog = self.elog
+            for level, msg in logs:
+                if level == logging.INFO:
+                    elog.log(level, msg)
+                elif msg.startswith("Failed to notify"):
+                    self.svc_log.error(msg)
+                else:
+                    self.log.error(msg)
+            elog.flush()
+        if lat:
+            self.metrics.latency.observe_many(array.array("q", lat))
+        for i in need_connect:
+            self._schedule_connect(i, failed=(i == connect_failed))
+        for i in want_write:
+            sock = self.socks.get(i)
+            if sock is not None and i not in self.writers:
+                self.writers.add(i)
+                self.loop.add_writer(sock.fileno(), self._writable, i)
+        pending = self.core.pending()
+        if not self.saturated and pending >= self.high_water:
+            self.saturated = True
+            if self.on_saturation:
+                self.on_saturation(True)
+        elif self.saturated and pending <= self.low_water:
+            self.saturated = False
+            if self.on_saturation:
+                self.on_saturation(False)
+
+    async def _watchdog_loop(self) -> None:
+        timeout_ns = int(self.settings.timeout * 1e9)
+        period = max(0.05, min(1.0, self.settings.timeout / 4))
+        while True:
+            await asyncio.sleep(period)
+            for i in self.core.check_timeouts(timeout_ns):
+                self.log.error(f"Timeout error: Request to {self.endpoint_url} timed out")
+                self._drop_socket(i)
+                self.core.detach(i, f"Timeout error: Request to {self.endpoint_url} timed out")
+            self._after()

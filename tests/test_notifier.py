@@ -10,6 +10,7 @@ import pytest
 from conftest import run
 from k8s_watcher_amd.metrics import Metrics
 from k8s_watcher_amd.models.payload import build_core
+from k8s_watcher_amd.parallel.native_notifier import NativeNotifierPool
 from k8s_watcher_amd.parallel.notifier import NotifierPool
 from k8s_watcher_amd.testing.stub_sink import StubSink
 from k8s_watcher_amd.utils.config import ClusterApiSettings, NotifierPoolSettings, RetryPolicy
@@ -30,11 +31,17 @@ def core(uid, phase="Running", name=None):
     return build_core(pod, "production")
 
 
-async def with_pool(sink_kwargs=None, **kw):
+@pytest.fixture(params=["python", "native"])
+def pool_cls(request):
+    """Every test runs against the asyncio pool and the native-core pool."""
+    return NotifierPool if request.param == "python" else NativeNotifierPool
+
+
+async def with_pool(cls, sink_kwargs=None, **kw):
     sink = StubSink(**(sink_kwargs or {}))
     await sink.start()
     m = Metrics(record_samples=True)
-    pool = NotifierPool(settings(sink.url, **kw), m)
+    pool = cls(settings(sink.url, **kw), m)
     return sink, pool, m
 
 
@@ -43,9 +50,9 @@ async def close(sink, pool):
     await sink.stop()
 
 
-def test_delivers_with_headers_and_latency():
+def test_delivers_with_headers_and_latency(pool_cls):
     async def body():
-        sink, pool, m = await with_pool(api_key="k3y")
+        sink, pool, m = await with_pool(pool_cls, api_key="k3y")
         for i in range(20):
             pool.submit(f"u{i}", "ADDED", "default", f"p{i}", core(f"u{i}"), 0, TS)
         pool.flush()
@@ -64,9 +71,9 @@ def test_delivers_with_headers_and_latency():
 
 
 @pytest.mark.parametrize("status", [201, 204])
-def test_any_2xx_is_success(status):
+def test_any_2xx_is_success(pool_cls, status):
     async def body():
-        sink, pool, m = await with_pool({"success_status": status})
+        sink, pool, m = await with_pool(pool_cls, {"success_status": status})
         pool.submit("u", "ADDED", "default", "p", core("u"), 0, TS)
         pool.flush()
         await pool.drain(5)
@@ -77,9 +84,9 @@ def test_any_2xx_is_success(status):
     assert m.c["notify_delivered"] == 1 and m.c["notify_failed"] == 0
 
 
-def test_5xx_retried_4xx_not():
+def test_5xx_retried_4xx_not(pool_cls):
     async def body():
-        sink, pool, m = await with_pool()
+        sink, pool, m = await with_pool(pool_cls)
         sink.state.fail_next = [500, 503]
         pool.submit("a", "ADDED", "default", "a", core("a"), 0, TS)
         pool.flush()
@@ -97,9 +104,9 @@ def test_5xx_retried_4xx_not():
     assert m.c["notify_retried"] == 2 and m.c["notify_failed"] == 1 and m.c["notify_delivered"] == 1
 
 
-def test_gives_up_after_max_attempts():
+def test_gives_up_after_max_attempts(pool_cls):
     async def body():
-        sink, pool, m = await with_pool({"fail_rate": 1.0}, attempts=3)
+        sink, pool, m = await with_pool(pool_cls, {"fail_rate": 1.0}, attempts=3)
         pool.submit("a", "ADDED", "default", "a", core("a"), 0, TS)
         pool.flush()
         assert await pool.drain(5)
@@ -110,9 +117,9 @@ def test_gives_up_after_max_attempts():
     assert failed == 3 and m.c["notify_failed"] == 1 and m.c["notify_retried"] == 2
 
 
-def test_timeout_aborts_and_retries():
+def test_timeout_aborts_and_retries(pool_cls):
     async def body():
-        sink, pool, m = await with_pool({"latency": 0.6}, timeout=0.2, attempts=2, delay=0.3)
+        sink, pool, m = await with_pool(pool_cls, {"latency": 0.6}, timeout=0.2, attempts=2, delay=0.3)
         pool.submit("a", "ADDED", "default", "a", core("a"), 0, TS)
         pool.flush()
         await asyncio.sleep(0.35)
@@ -125,9 +132,9 @@ def test_timeout_aborts_and_retries():
     assert m.c["notify_retried"] == 1 and m.c["notify_delivered"] == 1
 
 
-def test_stale_retry_is_superseded():
+def test_stale_retry_is_superseded(pool_cls):
     async def body():
-        sink, pool, m = await with_pool(connections=1, delay=0.2)
+        sink, pool, m = await with_pool(pool_cls, connections=1, delay=0.2)
         sink.state.fail_next = [503]
         pool.submit("u", "MODIFIED", "default", "p", core("u", "Running"), 0, TS)
         pool.flush()
@@ -144,9 +151,9 @@ def test_stale_retry_is_superseded():
     assert m.c["notify_superseded"] == 1
 
 
-def test_coalesce_replaces_unsent_body():
+def test_coalesce_replaces_unsent_body(pool_cls):
     async def body():
-        sink, pool, m = await with_pool(coalesce=True, connections=1)
+        sink, pool, m = await with_pool(pool_cls, coalesce=True, connections=1)
         for ph in ("Pending", "Running", "Succeeded"):
             pool.submit("u", "MODIFIED", "default", "p", core("u", ph), 0, TS)
         pool.flush()
@@ -161,12 +168,12 @@ def test_coalesce_replaces_unsent_body():
 
 
 @pytest.mark.parametrize("depth", [1, 8])
-def test_per_pod_order_under_random_failures(depth):
+def test_per_pod_order_under_random_failures(pool_cls, depth):
     rng = random.Random(3)
     order = ["Pending", "Running", "Succeeded"]
 
     async def body():
-        sink, pool, m = await with_pool({"fail_rate": 0.2, "fail_status": 503, "seed": 5},
+        sink, pool, m = await with_pool(pool_cls, {"fail_rate": 0.2, "fail_status": 503, "seed": 5},
                                         connections=4, depth=depth, attempts=8, delay=0.005)
         uids = [f"u{i}" for i in range(40)]
         steps = {u: 0 for u in uids}
@@ -193,13 +200,13 @@ def test_per_pod_order_under_random_failures(depth):
     assert m.c["notify_failed"] == 0
 
 
-def test_backpressure_signals():
+def test_backpressure_signals(pool_cls):
     flips = []
 
     async def body():
         sink = StubSink(latency=0.05)
         await sink.start()
-        pool = NotifierPool(settings(sink.url, queue_size=8, connections=2), Metrics(),
+        pool = pool_cls(settings(sink.url, queue_size=8, connections=2), Metrics(),
                             on_saturation=flips.append)
         for i in range(20):
             pool.submit(f"u{i}", "ADDED", "default", "p", core(f"u{i}"), 0, TS)
@@ -212,7 +219,7 @@ def test_backpressure_signals():
     assert flips == [True, False]
 
 
-def test_unreachable_sink_then_recovery():
+def test_unreachable_sink_then_recovery(pool_cls):
     async def body():
         import socket
         s = socket.socket()
@@ -220,7 +227,7 @@ def test_unreachable_sink_then_recovery():
         port = s.getsockname()[1]
         s.close()
         m = Metrics()
-        pool = NotifierPool(settings(f"http://127.0.0.1:{port}", attempts=2, delay=0.01), m)
+        pool = pool_cls(settings(f"http://127.0.0.1:{port}", attempts=2, delay=0.01), m)
         pool.submit("a", "ADDED", "default", "a", core("a"), 0, TS)
         pool.flush()
         assert await pool.drain(5)
@@ -238,12 +245,12 @@ def test_unreachable_sink_then_recovery():
     assert failed == 1 and n == 1
 
 
-def test_health_check():
+def test_health_check(pool_cls):
     async def body():
-        sink, pool, m = await with_pool()
+        sink, pool, m = await with_pool(pool_cls)
         ok = await pool.health_check()
         await close(sink, pool)
-        bad = NotifierPool(settings("http://127.0.0.1:1"), Metrics())
+        bad = pool_cls(settings("http://127.0.0.1:1"), Metrics())
         nok = await bad.health_check(timeout=1)
         await bad.close()
         return ok, nok
