@@ -52,12 +52,52 @@ class EventPipeline:
         self.log_events_setting = w.log_events
         self.shard = ShardFilter(w.shard)
         self.last_rv: Optional[str] = None
+        self.native = None
+        self._native_log = None
 
     @property
     def log_events(self) -> bool:
         if self.log_events_setting is not None:
             return self.log_events_setting
         return self.log.isEnabledFor(logging.INFO)
+
+    # ------------------------------------------------------------------ native fast path
+    def attach_native(self) -> None:
+        """Run watch batches through ``_kwcore.Pipeline`` (decode + this class's
+        per-event logic fused in C++), submitting straight into the native
+        notifier core when the pool has one. Relists still use :meth:`reconcile`.
+        """
+        from ..ops.native import load
+        w = self.settings.watcher
+        core = getattr(self.notifier, "core", None)
+        self.native = load().Pipeline(
+            self.settings.environment, self.cache.entries, self.metrics.c, self.namespaces or None,
+            self.critical_active, self.phase_mode, self.shard.count, self.shard.index, self.shard.by_uid,
+            w.event_timestamp == "utc", core, False, False)
+
+    def handle_raw(self, data: bytes, read_ns: int, framed: bool) -> List[tuple]:
+        """Native path: raw watch bytes (HTTP-chunk framed or not) → everything
+        :meth:`handle_batch` does. Returns the control events."""
+        native = self.native
+        log_events = self.log_events
+        flags = (log_events, log_events and self.elog.enabled(logging.DEBUG))
+        if flags != self._native_log:
+            native.set_log(*flags)
+            self._native_log = flags
+        ctrl, last_rv, logs, submits, ts = (native.feed_chunked if framed else native.feed)(data, read_ns)
+        if last_rv is not None:
+            self.last_rv = last_rv
+        elog = self.elog
+        if logs:
+            for level, msg in logs:
+                elog.log(level, msg)
+        if submits:
+            submit = self.notifier.submit
+            for uid, et, ns, name, core in submits:
+                submit(uid, et, ns, name, core, read_ns, ts)
+        self.notifier.flush()
+        elog.flush()
+        return ctrl
 
     def handle_batch(self, events: List[tuple], read_ns: int) -> List[tuple]:
         """Process decoded events; returns control events (ERROR/INVALID) for the reflector."""

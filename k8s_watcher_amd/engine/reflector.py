@@ -144,7 +144,20 @@ class Reflector:
         def on_mode(is_framed: bool) -> None:
             framed[0] = is_framed
 
+        native = pipeline.native
+        if native is not None:
+            native.reset()
+
         def sink(data: bytes, read_ns: int) -> None:
+            if native is not None:
+                ctrl = pipeline.handle_raw(data, read_ns, framed[0])
+                if pipeline.last_rv:
+                    self.rv = pipeline.last_rv
+                for ev in ctrl:
+                    self._handle_control(ev)
+                if framed[0] and native.body_done() and self.stream is not None:
+                    self.stream.close()  # server ended the watch (timeoutSeconds)
+                return
             if framed[0]:
                 evs = decoder.feed_chunked(data)
                 if decoder.body_done() and self.stream is not None:

@@ -165,6 +165,8 @@ class WatcherService:
                 saved_rvs, cache, _ = loaded
                 self.log.info(f"Resuming from checkpoint {ck}: {len(cache)} cached pods")
         self.pipeline = EventPipeline(s, self.decoder, self.notifier, self.metrics, cache, self.event_log)
+        if self._native_pipeline():
+            self.pipeline.attach_native()
         self.metrics.gauges["cached_pods"] = lambda: float(len(cache))
         self.metrics.gauges["notify_outstanding"] = lambda: float(self.notifier.outstanding())
         self.log.info(f"Starting Pod watcher in {s.environment} environment...")
@@ -195,7 +197,13 @@ class WatcherService:
         assert self.pipeline is not None
         p = EventPipeline(self.settings, decoder, self.notifier, self.metrics, self.pipeline.cache,
                           self.event_log)
+        if self._native_pipeline():
+            p.attach_native()
         return p
+
+    def _native_pipeline(self) -> bool:
+        w = self.settings.watcher
+        return w.engine == "native" and w.state_format == "structured"
 
     async def _wait_synced(self) -> None:
         synced = asyncio.ensure_future(asyncio.gather(*[r.synced.wait() for r in self.reflectors]))

@@ -1657,7 +1657,7 @@ PyMODINIT_FUNC PyInit__kwcore(void) {
     if (PyType_Ready(&ScannerType) < 0) return nullptr;
     Py_INCREF(&ScannerType);
     PyModule_AddObject(m, "ResponseScanner", (PyObject*)&ScannerType);
-    if (register_engine(m) < 0) return nullptr;
+    if (register_engine(m) < 0 || register_pipeline(m) < 0) return nullptr;
     const char* names[6] = {"ADDED", "MODIFIED", "DELETED", "BOOKMARK", "ERROR", "INVALID"};
     for (int i = 0; i < 6; ++i) {
         g_types[i] = PyUnicode_InternFromString(names[i]);
