@@ -257,7 +257,7 @@ async def config1(a) -> dict:
 
 
 async def config2(a) -> dict:
-    steps = max(2, int(10 * a.scale))
+    steps = max(2, int(100 * a.scale))  # 300 events per step: many steps for a stable rate
     async with Servers("createdelete", 100, prerender=steps + 1) as srv:
         e = srv.events_per_step
         ours = await run_ours(srv, "development", {}, [f"STEP {k}" for k in range(1, steps + 1)],
@@ -268,7 +268,7 @@ async def config2(a) -> dict:
 
 
 async def config3(a) -> dict:
-    steps = max(2, int(10 * a.scale))
+    steps = max(2, int(50 * a.scale))
     ov = {"watcher": {"namespaces": ["default"], "namespace_scope": "server"}}
     async with Servers("steady", 1000, prerender=steps + 1, namespaces="default") as srv:
         ours = await run_ours(srv, "staging", ov, [f"STEP {k}" for k in range(1, steps + 1)], ["STEP 0"],
