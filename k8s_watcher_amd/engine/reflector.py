@@ -118,9 +118,9 @@ class Reflector:
 
     # ------------------------------------------------------------------ watch
     def _handle_control(self, ev: tuple) -> None:
-        if ev[E_TYPE] == INVALID:
+        if ev[E_TYPE] != ERROR:  # INVALID line or an event type this watcher does not know
             self.metrics.c["events_invalid"] += 1
-            self.log.warning(f"Skipping undecodable watch line: {ev[E_EXTRA]}")
+            self.log.warning(f"Skipping undecodable watch line ({ev[E_TYPE]}): {ev[E_EXTRA]}")
             return
         status = ev[E_EXTRA] or {}
         code = status.get("code")

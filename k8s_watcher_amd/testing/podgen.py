@@ -12,7 +12,6 @@ matter at scale.
 
 from __future__ import annotations
 
-import copy
 import datetime as _dt
 import json
 import random

@@ -5,8 +5,6 @@ Ten ADDED pods across namespaces; the development profile filters to
 the §2.3 schema, in order.
 """
 
-import asyncio
-
 import pytest
 
 from conftest import run

@@ -1,7 +1,5 @@
 """HTTP/1.1 response parser edge cases and the metrics endpoint."""
 
-import asyncio
-
 import pytest
 
 from conftest import run

@@ -1,10 +1,8 @@
 """Kubeconfig / in-cluster loading and TLS end to end."""
 
 import base64
-import json
 import os
 import ssl
-import stat
 import sys
 import textwrap
 

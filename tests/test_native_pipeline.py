@@ -11,7 +11,7 @@ from k8s_watcher_amd.engine.pipeline import EventPipeline
 from k8s_watcher_amd.metrics import Metrics
 from k8s_watcher_amd.ops.decode import PyDecoder
 from k8s_watcher_amd.testing.podgen import churn_events, event_line
-from k8s_watcher_amd.utils.config import deep_merge, load_settings
+from k8s_watcher_amd.utils.config import load_settings
 
 
 class Recorder:

@@ -2,7 +2,6 @@
 timeouts, per-pod ordering, superseding, coalescing and backpressure."""
 
 import asyncio
-import json
 import random
 
 import pytest

@@ -13,7 +13,7 @@ import time
 
 import pytest
 
-from conftest import ROOT, run
+from conftest import ROOT
 from k8s_watcher_amd.parallel.shard import ShardFilter, shard_of
 from k8s_watcher_amd.testing.fake_apiserver import FakeApiServer, ServerThread
 from k8s_watcher_amd.testing.podgen import PodFactory
