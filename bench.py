@@ -59,6 +59,7 @@ def parse_args(argv=None):
     ap.add_argument("--engine", default="native", choices=["native", "python"])
     ap.add_argument("--connections", type=int, default=None, help="notifier pool connections")
     ap.add_argument("--pipeline-depth", type=int, default=None)
+    ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
     ap.add_argument("--sink-workers", type=int, default=4)
     ap.add_argument("--latency-rate", type=float, default=100.0)
     ap.add_argument("--latency-seconds", type=float, default=3.0)
@@ -148,6 +149,8 @@ async def rank_main(args, d: Dist) -> dict:
             pool["connections"] = args.connections
         if args.pipeline_depth:
             pool["pipeline_depth"] = args.pipeline_depth
+        if args.python_pool:
+            pool["native"] = False
         if pool:
             overrides["clusterapi"]["pool"] = pool
         settings = load_settings(args.profile, overrides=overrides)

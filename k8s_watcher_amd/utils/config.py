@@ -209,6 +209,7 @@ class NotifierPoolSettings:
     pipeline_depth: int = 1
     queue_size: int = 65536
     coalesce: bool = False
+    native: bool = True  # C++ notifier core for http:// endpoints (watcher.engine: native)
 
 
 @dataclass
@@ -374,6 +375,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
             pipeline_depth=max(1, _as_int(pool.get("pipeline_depth", 1), "clusterapi.pool.pipeline_depth")),
             queue_size=max(1, _as_int(pool.get("queue_size", 65536), "clusterapi.pool.queue_size")),
             coalesce=_as_bool(pool.get("coalesce", False), "clusterapi.pool.coalesce"),
+            native=_as_bool(pool.get("native", True), "clusterapi.pool.native"),
         ),
         verify_tls=_as_bool(c.get("verify_tls", True), "clusterapi.verify_tls"),
         ca_file=c.get("ca_file") or None,
