@@ -63,9 +63,12 @@ struct PodSpans {
     Span phase;
     std::vector<Condition> conditions;
     std::vector<CStatus> cstatuses;
+    bool deferred = false;             // parse_pod_light: spec/arrays not walked yet
+    Span spec_raw, cond_raw, cstat_raw;
     void clear() {
-        meta_present = spec_present = status_present = false;
+        meta_present = spec_present = status_present = deferred = false;
         name = ns = uid = rv = labels = annotations = ctime = node_name = phase = Span();
+        spec_raw = cond_raw = cstat_raw = Span();
         containers.clear();
         conditions.clear();
         cstatuses.clear();
@@ -119,6 +122,7 @@ class Parser {
 
 #if defined(__x86_64__)
     static bool use_avx2;
+    static bool use_avx512;
     __attribute__((target("avx2,bmi,bmi2"))) const char* string_end_avx2(const char* s) {
         const __m256i q = _mm256_set1_epi8('"');
         const __m256i bs = _mm256_set1_epi8('\\');
@@ -177,7 +181,7 @@ class Parser {
         alignas(32) char tail[64];
         const __m256i vq = _mm256_set1_epi8('"'), vb = _mm256_set1_epi8('\\');
         const __m256i vob = _mm256_set1_epi8('{'), vcb = _mm256_set1_epi8('}');
-        const __m256i vos = _mm256_set1_epi8('['), vcs = _mm256_set1_epi8(']');
+        const __m256i v20 = _mm256_set1_epi8(0x20);
         while (p < end_) {
             size_t avail = (size_t)(end_ - p);
             const char* blk = p;
@@ -195,8 +199,62 @@ class Parser {
                 _mm_clmulepi64_si128(_mm_set_epi64x(0, (long long)quotes), _mm_set1_epi8((char)0xFF), 0));
             in_str ^= prev_in_string;
             prev_in_string = (uint64_t)((int64_t)in_str >> 63);
-            uint64_t open = (mask64(lo, hi, vob) | mask64(lo, hi, vos)) & ~in_str & valid;
-            uint64_t close = (mask64(lo, hi, vcb) | mask64(lo, hi, vcs)) & ~in_str & valid;
+            // '{'|0x20 == '['|0x20 == '{' and '}'|0x20 == ']'|0x20 == '}': one compare per bracket kind
+            const __m256i lo20 = _mm256_or_si256(lo, v20), hi20 = _mm256_or_si256(hi, v20);
+            uint64_t open = mask64(lo20, hi20, vob) & ~in_str & valid;
+            uint64_t close = mask64(lo20, hi20, vcb) & ~in_str & valid;
+            int64_t nclose = __builtin_popcountll(close);
+            if (depth > nclose) {
+                depth += __builtin_popcountll(open) - nclose;
+            } else {
+                uint64_t m = open | close;
+                while (m) {
+                    int i = __builtin_ctzll(m);
+                    if ((open >> i) & 1) {
+                        ++depth;
+                    } else if (--depth == 0) {
+                        return p + i + 1;
+                    }
+                    m &= m - 1;
+                }
+            }
+            p += avail < 64 ? avail : 64;
+        }
+        fail("unterminated container");
+    }
+
+    // AVX-512BW form of the same block scanner (Zen 4/5 and recent Xeons run
+    // 512-bit compares at full width): one load and four compares yield the
+    // 64-bit quote/backslash/open/close masks directly in mask registers, the
+    // escape pass is skipped for blocks with no backslash, and the final
+    // partial block is a fault-suppressing masked load instead of a copy.
+    __attribute__((target("avx512f,avx512bw,bmi,bmi2,pclmul,popcnt"))) const char* skip_container_512(
+        const char* s) {
+        uint64_t prev_escaped = 0, prev_in_string = 0;
+        int64_t depth = 0;
+        const char* p = s;
+        const __m512i vq = _mm512_set1_epi8('"'), vb = _mm512_set1_epi8('\\');
+        const __m512i vo = _mm512_set1_epi8('{'), vc = _mm512_set1_epi8('}'), v20 = _mm512_set1_epi8(0x20);
+        while (p < end_) {
+            size_t avail = (size_t)(end_ - p);
+            uint64_t valid = ~0ULL;
+            __m512i v;
+            if (avail >= 64) {
+                v = _mm512_loadu_si512(reinterpret_cast<const void*>(p));
+            } else {
+                valid = (1ULL << avail) - 1;
+                v = _mm512_maskz_loadu_epi8(valid, p);
+            }
+            uint64_t quotes = _mm512_cmpeq_epi8_mask(v, vq);
+            uint64_t bs = _mm512_cmpeq_epi8_mask(v, vb);
+            if (bs | prev_escaped) quotes &= ~escaped_mask(bs, prev_escaped);
+            uint64_t in_str = (uint64_t)_mm_cvtsi128_si64(
+                _mm_clmulepi64_si128(_mm_set_epi64x(0, (long long)quotes), _mm_set1_epi8((char)0xFF), 0));
+            in_str ^= prev_in_string;
+            prev_in_string = (uint64_t)((int64_t)in_str >> 63);
+            const __m512i f = _mm512_or_si512(v, v20);
+            uint64_t open = _mm512_cmpeq_epi8_mask(f, vo) & ~in_str & valid;
+            uint64_t close = _mm512_cmpeq_epi8_mask(f, vc) & ~in_str & valid;
             int64_t nclose = __builtin_popcountll(close);
             if (depth > nclose) {
                 depth += __builtin_popcountll(open) - nclose;
@@ -304,7 +362,9 @@ class Parser {
             p_ = string_end(p_);
         } else if (c == '{' || c == '[') {
 #if defined(__x86_64__)
-            p_ = use_avx2 ? skip_container_blocks(p_) : skip_container_scalar(p_, 0);
+            p_ = use_avx512 ? skip_container_512(p_)
+                 : use_avx2 ? skip_container_blocks(p_)
+                            : skip_container_scalar(p_, 0);
 #else
             p_ = skip_container_scalar(p_, 0);
 #endif
@@ -378,11 +438,17 @@ class Parser {
 
 #if defined(__x86_64__)
 bool Parser::use_avx2 = false;
+bool Parser::use_avx512 = false;
 
 bool simd_supported() {
     __builtin_cpu_init();
     return __builtin_cpu_supports("avx2") && __builtin_cpu_supports("bmi2") &&
            __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("popcnt");
+}
+
+bool avx512_supported() {
+    __builtin_cpu_init();
+    return simd_supported() && __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw");
 }
 #endif
 
@@ -419,30 +485,65 @@ void parse_metadata(Parser& P, PodSpans& S) {
     });
 }
 
+void parse_containers(Parser& P, PodSpans& S) {
+    if (P.null_here()) return;
+    if (P.peek() != '[') { P.value(); return; }
+    S.containers.clear();  // duplicate key: last wins
+    P.array([&]() {
+        if (P.peek() != '{') { P.value(); return; }
+        Container c;
+        P.object([&](const char* k, size_t kn) {
+            if (KEYIS("name")) c.name = P.value();
+            else if (KEYIS("image")) c.image = P.value();
+            else P.value();
+        });
+        S.containers.push_back(c);
+    });
+}
+
+void parse_conditions(Parser& P, PodSpans& S) {
+    if (P.null_here()) return;
+    if (P.peek() != '[') { P.value(); return; }
+    S.conditions.clear();
+    P.array([&]() {
+        if (P.peek() != '{') { P.value(); return; }
+        Condition c;
+        P.object([&](const char* k, size_t kn) {
+            if (KEYIS("type")) c.type = P.value();
+            else if (KEYIS("status")) c.status = P.value();
+            else if (KEYIS("reason")) c.reason = P.value();
+            else if (KEYIS("message")) c.message = P.value();
+            else P.value();
+        });
+        S.conditions.push_back(c);
+    });
+}
+
+void parse_cstatuses(Parser& P, PodSpans& S) {
+    if (P.null_here()) return;
+    if (P.peek() != '[') { P.value(); return; }
+    S.cstatuses.clear();
+    P.array([&]() {
+        if (P.peek() != '{') { P.value(); return; }
+        CStatus c;
+        P.object([&](const char* k, size_t kn) {
+            if (KEYIS("name")) c.name = P.value();
+            else if (KEYIS("ready")) c.ready = P.value();
+            else if (KEYIS("restartCount")) c.restart_count = P.value();
+            else if (KEYIS("state")) c.state = P.value();
+            else P.value();
+        });
+        S.cstatuses.push_back(c);
+    });
+}
+
 void parse_spec(Parser& P, PodSpans& S) {
     if (P.null_here()) return;
     S.spec_present = true;
     P.object([&](const char* k, size_t kn) {
-        if (KEYIS("nodeName")) {
-            S.node_name = P.value();
-        } else if (KEYIS("containers")) {
-            if (P.null_here()) return;
-            if (P.peek() != '[') { P.value(); return; }
-            S.containers.clear();  // duplicate key: last wins
-            P.array([&]() {
-                if (P.peek() != '{') { P.value(); return; }
-                Container c;
-                P.object([&](const char* k2, size_t kn2) {
-                    const char* k = k2; size_t kn = kn2;
-                    if (KEYIS("name")) c.name = P.value();
-                    else if (KEYIS("image")) c.image = P.value();
-                    else P.value();
-                });
-                S.containers.push_back(c);
-            });
-        } else {
-            P.value();
-        }
+        if (KEYIS("nodeName")) S.node_name = P.value();
+        else if (KEYIS("containers")) parse_containers(P, S);
+        else P.value();
     });
 }
 
@@ -450,45 +551,10 @@ void parse_status(Parser& P, PodSpans& S) {
     if (P.null_here()) return;
     S.status_present = true;
     P.object([&](const char* k, size_t kn) {
-        if (KEYIS("phase")) {
-            S.phase = P.value();
-        } else if (KEYIS("conditions")) {
-            if (P.null_here()) return;
-            if (P.peek() != '[') { P.value(); return; }
-            S.conditions.clear();
-            P.array([&]() {
-                if (P.peek() != '{') { P.value(); return; }
-                Condition c;
-                P.object([&](const char* k2, size_t kn2) {
-                    const char* k = k2; size_t kn = kn2;
-                    if (KEYIS("type")) c.type = P.value();
-                    else if (KEYIS("status")) c.status = P.value();
-                    else if (KEYIS("reason")) c.reason = P.value();
-                    else if (KEYIS("message")) c.message = P.value();
-                    else P.value();
-                });
-                S.conditions.push_back(c);
-            });
-        } else if (KEYIS("containerStatuses")) {
-            if (P.null_here()) return;
-            if (P.peek() != '[') { P.value(); return; }
-            S.cstatuses.clear();
-            P.array([&]() {
-                if (P.peek() != '{') { P.value(); return; }
-                CStatus c;
-                P.object([&](const char* k2, size_t kn2) {
-                    const char* k = k2; size_t kn = kn2;
-                    if (KEYIS("name")) c.name = P.value();
-                    else if (KEYIS("ready")) c.ready = P.value();
-                    else if (KEYIS("restartCount")) c.restart_count = P.value();
-                    else if (KEYIS("state")) c.state = P.value();
-                    else P.value();
-                });
-                S.cstatuses.push_back(c);
-            });
-        } else {
-            P.value();
-        }
+        if (KEYIS("phase")) S.phase = P.value();
+        else if (KEYIS("conditions")) parse_conditions(P, S);
+        else if (KEYIS("containerStatuses")) parse_cstatuses(P, S);
+        else P.value();
     });
 }
 
@@ -504,6 +570,62 @@ void parse_pod(Parser& P, PodSpans& S) {
             P.value();
         }
     });
+}
+
+// Filter-first variant for the fused pipeline: everything the filters and the
+// cache need (metadata, status.phase) is extracted, while spec and the two
+// status arrays are only bracket-skipped by the block scanner and their raw
+// spans kept; materialize() walks them later for the events that actually get
+// a payload. With the critical-events filter ~4 of 5 churn events never pay
+// for the container/condition walk.
+void parse_status_light(Parser& P, PodSpans& S) {
+    if (P.null_here()) return;
+    S.status_present = true;
+    P.object([&](const char* k, size_t kn) {
+        if (KEYIS("phase")) S.phase = P.value();
+        else if (KEYIS("conditions")) S.cond_raw = P.value();
+        else if (KEYIS("containerStatuses")) S.cstat_raw = P.value();
+        else P.value();
+    });
+}
+
+void parse_pod_light(Parser& P, PodSpans& S) {
+    S.deferred = true;
+    P.object([&](const char* k, size_t kn) {
+        if (KEYIS("metadata")) {
+            if (P.peek() == '{' || P.peek() == 'n') parse_metadata(P, S); else P.value();
+        } else if (KEYIS("spec")) {
+            char c = P.peek();
+            if (c == '{') {
+                S.spec_present = true;
+                S.spec_raw = P.value();
+            } else if (!P.null_here()) {
+                P.value();
+            }
+        } else if (KEYIS("status")) {
+            if (P.peek() == '{' || P.peek() == 'n') parse_status_light(P, S); else P.value();
+        } else {
+            P.value();
+        }
+    });
+}
+
+// Walk the sub-trees parse_pod_light deferred; throws ParseError like parse_pod.
+void materialize(PodSpans& S) {
+    if (!S.deferred) return;
+    S.deferred = false;
+    if (S.spec_raw.present()) {
+        Parser Q(S.spec_raw.p, S.spec_raw.p + S.spec_raw.n);
+        parse_spec(Q, S);
+    }
+    if (S.cond_raw.present()) {
+        Parser Q(S.cond_raw.p, S.cond_raw.p + S.cond_raw.n);
+        parse_conditions(Q, S);
+    }
+    if (S.cstat_raw.present()) {
+        Parser Q(S.cstat_raw.p, S.cstat_raw.p + S.cstat_raw.n);
+        parse_cstatuses(Q, S);
+    }
 }
 
 // ----------------------------------------------------------------------------- output
@@ -1551,16 +1673,21 @@ PyObject* kw_event_timestamp(PyObject*, PyObject* arg) {
 
 PyObject* kw_cpu_features(PyObject*, PyObject*) {
 #if defined(__x86_64__)
-    return Py_BuildValue("{s:O}", "avx2", Parser::use_avx2 ? Py_True : Py_False);
+    return Py_BuildValue("{s:O,s:O}", "avx2", Parser::use_avx2 ? Py_True : Py_False, "avx512",
+                         Parser::use_avx512 ? Py_True : Py_False);
 #else
-    return Py_BuildValue("{s:O}", "avx2", Py_False);
+    return Py_BuildValue("{s:O,s:O}", "avx2", Py_False, "avx512", Py_False);
 #endif
 }
 
+// set_simd(True) = best supported level, False = scalar, "avx2" = cap at AVX2.
 PyObject* kw_set_simd(PyObject*, PyObject* arg) {
 #if defined(__x86_64__)
+    bool cap_avx2 = PyUnicode_Check(arg) && PyUnicode_CompareWithASCIIString(arg, "avx2") == 0;
     int on = PyObject_IsTrue(arg);
+    if (on < 0) return nullptr;
     Parser::use_avx2 = on && simd_supported();
+    Parser::use_avx512 = on && !cap_avx2 && avx512_supported();
 #endif
     Py_RETURN_NONE;
 }
@@ -1568,7 +1695,8 @@ PyObject* kw_set_simd(PyObject*, PyObject* arg) {
 // bench_parse(data, mode, repeat) -> seconds. Times the pure C++ stages on
 // newline-separated lines without creating Python objects:
 // mode 0 = structural skip of each line, 1 = field extraction (spans),
-// 2 = extraction + payload core assembly.
+// 2 = extraction + payload core assembly, 3 = filter-first light extraction,
+// 4 = light extraction + materialize + core assembly.
 PyObject* kw_bench_parse(PyObject*, PyObject* args) {
     Py_buffer view;
     int mode = 2, repeat = 1;
@@ -1598,10 +1726,16 @@ PyObject* kw_bench_parse(PyObject*, PyObject* args) {
                     continue;
                 }
                 S.clear();
+                const bool light = mode >= 3;
                 P.object([&](const char* k, size_t kn) {
-                    if (KEYIS("object")) parse_pod(P, S); else P.value();
+                    if (KEYIS("object")) {
+                        if (light) parse_pod_light(P, S); else parse_pod(P, S);
+                    } else {
+                        P.value();
+                    }
                 });
-                if (mode >= 2) {
+                if (mode == 2 || mode == 4) {
+                    materialize(S);
                     build_core(out, S, env);
                     sink += out.size();
                 } else {
@@ -1671,6 +1805,7 @@ PyMODINIT_FUNC PyInit__kwcore(void) {
 #if defined(__x86_64__)
     __builtin_cpu_init();
     Parser::use_avx2 = simd_supported();
+    Parser::use_avx512 = avx512_supported();
 #endif
     return m;
 }

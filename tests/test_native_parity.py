@@ -135,16 +135,18 @@ def test_core_from_summary_parity():
 
 
 def test_scalar_and_simd_paths_agree():
+    """Scalar, AVX2 and (where the CPU has it) AVX-512BW block scanners decode
+    the same stream to the same events, with and without the light pipeline."""
     mod = load()
     data = b"".join(event_line(t, o) for t, o in churn_events(50, seed=8))
-    mod.set_simd(True)
-    simd = NativeDecoder(ENV).feed(data)
-    mod.set_simd(False)
+    results = []
     try:
-        scalar = NativeDecoder(ENV).feed(data)
+        for level in (False, "avx2", True):
+            mod.set_simd(level)
+            results.append([s[:8] for s in NativeDecoder(ENV).feed(data)])
     finally:
         mod.set_simd(True)
-    assert [s[:8] for s in simd] == [s[:8] for s in scalar]
+    assert results[0] == results[1] == results[2]
 
 
 def test_environment_is_json_escaped():
@@ -197,3 +199,32 @@ def test_fuzz_parity(obj, etype, ascii_, spaced):
         assert (x[i] if isinstance(x[i], str) else None) == y[i]
     assert x[6] == y[6]
     assert json.loads(py.core(x)) == json.loads(nat.core(y))
+
+
+# Strings full of brackets, quotes and backslash runs, nested to random depth:
+# the block scanners must find the same container end at every SIMD level.
+_tricky = st.text(alphabet='{}[]"\\\\ ab:,', min_size=0, max_size=90)
+_nested = st.recursive(
+    _tricky | st.integers() | st.booleans() | st.none(),
+    lambda ch: st.lists(ch, max_size=5) | st.dictionaries(_tricky, ch, max_size=5),
+    max_leaves=25)
+
+
+@settings(max_examples=150, deadline=None)
+@given(skipme=_nested, pad=st.integers(min_value=0, max_value=130))
+def test_fuzz_block_skipper_all_levels(skipme, pad):
+    obj = {"metadata": {"name": "p", "namespace": "default", "uid": "u", "resourceVersion": "1",
+                        "labels": {"x" * pad: skipme}, "junk": [skipme, {"a": skipme}]},
+           "spec": {"volumes": skipme, "containers": [{"name": "c", "image": "i", "env": skipme}]},
+           "status": {"phase": "Running", "junk": skipme}}
+    line = json.dumps({"type": "MODIFIED", "object": obj}).encode() + b"\n"
+    mod = load()
+    out = []
+    try:
+        for level in (False, "avx2", True):
+            mod.set_simd(level)
+            out.append([e[:8] for e in NativeDecoder(ENV).feed(line)])
+    finally:
+        mod.set_simd(True)
+    assert out[0] == out[1] == out[2]
+    assert out[0] and out[0][0][0] == "MODIFIED"

@@ -112,3 +112,18 @@ def test_native_pipeline_logs_like_python():
     p.handle_raw(ev, 0, framed=False)
     assert lines == [(20, "Pod event detected: ADDED - batch/a")] + \
         ([(10, "Skipping pod batch/a - not in target namespaces")] if p.elog.enabled(10) else [])
+
+
+def test_light_parse_defers_payload_subtrees():
+    """With a filter active the pipeline only walks spec/status arrays for events
+    that get a payload: a malformed container list is reported (INVALID) on an
+    event that passes the critical filter and never looked at on one that does not."""
+    bad_spec = b'"spec":{"containers":[{"name" "c"}]}'
+    keep = (b'{"type":"DELETED","object":{"metadata":{"name":"a","namespace":"default","uid":"u1",'
+            b'"resourceVersion":"5"},' + bad_spec + b',"status":{"phase":"Running"}}}\n')
+    drop = (b'{"type":"MODIFIED","object":{"metadata":{"name":"b","namespace":"default","uid":"u2",'
+            b'"resourceVersion":"6"},' + bad_spec + b',"status":{"phase":"Running"}}}\n')
+    calls, entries, c, last_rv, ctrl = run_native("production", {}, keep + drop)
+    assert ctrl == ["INVALID"]
+    assert calls == []
+    assert c["events_filtered_critical"] == 1 and "u2" in entries and last_rv == "6"
