@@ -59,6 +59,7 @@ def parse_args(argv=None):
     ap.add_argument("--engine", default="native", choices=["native", "python"])
     ap.add_argument("--connections", type=int, default=None, help="notifier pool connections")
     ap.add_argument("--pipeline-depth", type=int, default=None)
+    ap.add_argument("--decode-threads", default=None, help="watcher.decode_threads (int or auto)")
     ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
     ap.add_argument("--sink-workers", type=int, default=4)
     ap.add_argument("--latency-rate", type=float, default=100.0)
@@ -142,7 +143,8 @@ async def rank_main(args, d: Dist) -> dict:
         overrides = {
             "clusterapi": {"base_url": f"http://127.0.0.1:{sink_port}", "timeout": 30,
                            "enabled": not os.environ.get("BENCH_NO_NOTIFY")},
-            "watcher": {"engine": args.engine, "retry": {"max_attempts": 0, "delay_seconds": 0.05}},
+            "watcher": {"engine": args.engine, "retry": {"max_attempts": 0, "delay_seconds": 0.05},
+                        **({"decode_threads": args.decode_threads} if args.decode_threads is not None else {})},
         }
         pool = {}
         if args.connections:
@@ -166,6 +168,8 @@ async def rank_main(args, d: Dist) -> dict:
             await asyncio.sleep(0.01)
 
         c = metrics.c
+        native_pl = svc.pipeline.native if svc.pipeline is not None else None
+        decode_threads = native_pl.decode_threads() if native_pl is not None else None
 
         debug = bool(os.environ.get("BENCH_DEBUG"))
 
@@ -193,10 +197,12 @@ async def rank_main(args, d: Dist) -> dict:
         metrics.latency.reset()
         d.barrier()
         n0, s0 = c["events_received"], c["notify_delivered"]
+        cpu0 = cpu_snapshot(replay.pid, sink.pid)
         t0 = time.perf_counter()
         for k in range(args.warmup, args.warmup + args.steps):
             await run_step(k)
         elapsed = time.perf_counter() - t0
+        cpu1 = cpu_snapshot(replay.pid, sink.pid)
         d.barrier()
         events = c["events_received"] - n0
         notified = c["notify_delivered"] - s0
@@ -220,7 +226,9 @@ async def rank_main(args, d: Dist) -> dict:
         await replay.stdin.drain()
         return {"elapsed": elapsed, "events": events, "notified": notified, "events_per_step": events_per_step,
                 "p50_ns": p50, "p99_ns": p99, "lat_samples": lat_n, "sat_p50_ns": sat_p50,
-                "failed": failed, "ref": ref}
+                "failed": failed, "ref": ref,
+                "cpu_util": {k: round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0},
+                "decode_threads": decode_threads}
     finally:
         for p in (replay, sink):
             try:
@@ -237,6 +245,30 @@ async def rank_main(args, d: Dist) -> dict:
             transport = getattr(p, "_transport", None)
             if transport is not None:
                 transport.close()  # close pipes while the loop is alive (no __del__ noise)
+
+
+def cpu_snapshot(replay_pid: int, sink_pid: int) -> dict:
+    """CPU seconds (user+system) of this watcher process and of the replay and
+    sink process trees — which side saturates a core tells what bounds a run."""
+    import psutil
+
+    def tree(pid: int) -> float:
+        try:
+            root = psutil.Process(pid)
+            procs = [root] + root.children(recursive=True)
+        except psutil.NoSuchProcess:
+            return 0.0
+        tot = 0.0
+        for pr in procs:
+            try:
+                t = pr.cpu_times()
+                tot += t.user + t.system
+            except psutil.NoSuchProcess:
+                pass
+        return tot
+
+    t = os.times()
+    return {"watcher": t.user + t.system, "replay": tree(replay_pid), "sink": tree(sink_pid)}
 
 
 async def run_reference(args, api_port: int, sink_port: int, cmd, step: int) -> dict:
@@ -311,6 +343,7 @@ def main(argv=None) -> int:
             "seq_len": None,
             "parallelism": f"shard{d.world}" if d.world > 1 else "single-process",
             "engine": args.engine,
+            "decode_threads": res["decode_threads"],
         },
         "p50_latency_ms": round(p50 / 1e6, 3) if p50 else None,
         "p99_latency_ms": round(p99 / 1e6, 3) if p99 else None,
@@ -318,6 +351,7 @@ def main(argv=None) -> int:
         "latency_samples": res["lat_samples"],
         "notified_per_s": round(notified / elapsed, 1),
         "notify_failed": res["failed"],
+        "cpu_util_rank0": res["cpu_util"],
         "saturated_p50_latency_ms": round(res["sat_p50_ns"] / 1e6, 3) if res["sat_p50_ns"] else None,
         "reference_equiv": ({"events_per_s": round(ref_rate, 1), "events": ref["events"],
                              "notified": ref["notified"],

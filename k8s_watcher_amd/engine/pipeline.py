@@ -62,18 +62,25 @@ class EventPipeline:
         return self.log.isEnabledFor(logging.INFO)
 
     # ------------------------------------------------------------------ native fast path
-    def attach_native(self) -> None:
+    def attach_native(self, decode_pool=None) -> None:
         """Run watch batches through ``_kwcore.Pipeline`` (decode + this class's
         per-event logic fused in C++), submitting straight into the native
         notifier core when the pool has one. Relists still use :meth:`reconcile`.
+
+        Line decoding fans out over ``decode_pool`` (a ``_kwcore.DecodePool``
+        shared by every scope's pipeline) or, without one, a private pool of
+        ``watcher.decode_threads`` workers (``auto``: utils/cpus.py).
         """
         from ..ops.native import load
+        from ..utils.cpus import auto_decode_threads
         w = self.settings.watcher
         core = getattr(self.notifier, "core", None)
+        decode = decode_pool if decode_pool is not None else (
+            w.decode_threads if w.decode_threads >= 0 else auto_decode_threads())
         self.native = load().Pipeline(
             self.settings.environment, self.cache.entries, self.metrics.c, self.namespaces or None,
             self.critical_active, self.phase_mode, self.shard.count, self.shard.index, self.shard.by_uid,
-            w.event_timestamp == "utc", core, False, False)
+            w.event_timestamp == "utc", core, False, False, decode)
 
     def handle_raw(self, data: bytes, read_ns: int, framed: bool) -> List[tuple]:
         """Native path: raw watch bytes (HTTP-chunk framed or not) → everything

@@ -60,6 +60,7 @@ class WatcherService:
         self.api: Optional[KubeApi] = None
         self.notifier = None
         self.pipeline: Optional[EventPipeline] = None
+        self._decode_pool = None
         self.reflectors: List[Reflector] = []
         self.decoder = None
         self._stop = asyncio.Event()
@@ -166,7 +167,8 @@ class WatcherService:
                 self.log.info(f"Resuming from checkpoint {ck}: {len(cache)} cached pods")
         self.pipeline = EventPipeline(s, self.decoder, self.notifier, self.metrics, cache, self.event_log)
         if self._native_pipeline():
-            self.pipeline.attach_native()
+            self._decode_pool = self._make_decode_pool()
+            self.pipeline.attach_native(self._decode_pool)
         self.metrics.gauges["cached_pods"] = lambda: float(len(cache))
         self.metrics.gauges["notify_outstanding"] = lambda: float(self.notifier.outstanding())
         self.log.info(f"Starting Pod watcher in {s.environment} environment...")
@@ -198,8 +200,16 @@ class WatcherService:
         p = EventPipeline(self.settings, decoder, self.notifier, self.metrics, self.pipeline.cache,
                           self.event_log)
         if self._native_pipeline():
-            p.attach_native()
+            p.attach_native(self._decode_pool)
         return p
+
+    def _make_decode_pool(self):
+        """One decode pool for every watch scope (they share the loop thread)."""
+        from ..ops.native import load
+        from ..utils.cpus import auto_decode_threads
+        w = self.settings.watcher
+        n = w.decode_threads if w.decode_threads >= 0 else auto_decode_threads()
+        return load().DecodePool(n) if n > 0 else 0
 
     def _native_pipeline(self) -> bool:
         w = self.settings.watcher

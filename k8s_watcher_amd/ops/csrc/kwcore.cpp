@@ -18,11 +18,14 @@
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 
+#include <linux/futex.h>
 #include <sys/socket.h>
+#include <sys/syscall.h>
 #include <sys/types.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cmath>
 #include <cstdint>
@@ -30,6 +33,7 @@
 #include <ctime>
 #include <deque>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 

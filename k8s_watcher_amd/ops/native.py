@@ -35,7 +35,7 @@ def compiler() -> str:
 
 def build_command() -> list:
     inc = sysconfig.get_paths()["include"]
-    return [compiler(), "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
+    return [compiler(), "-O3", "-std=c++17", "-pthread", "-fPIC", "-shared", "-fvisibility=hidden",
             "-fno-strict-aliasing", "-Wall", "-Wno-shadow", "-Wno-unused-function", "-Wno-psabi",
             f"-I{inc}", f"-I{os.path.dirname(SRC)}", SRC, "-o", SO]
 

@@ -256,6 +256,7 @@ class WatcherSettings:
     list_page_size: int = 500
     watch_interval: float = 1.0  # accepted for schema parity; a watch has no poll interval
     engine: str = "native"  # native | python
+    decode_threads: int = -1  # native engine: extra watch-decode threads, -1 = auto (utils/cpus.py)
     state_format: str = "structured"  # structured | python_repr
     event_timestamp: str = "local"  # local | utc
     log_events: Optional[bool] = None  # None = follow log level (parity)
@@ -311,6 +312,15 @@ def _shard(block: Dict[str, Any]) -> ShardSettings:
     return s
 
 
+def _decode_threads(v: Any) -> int:
+    if v is None or (isinstance(v, str) and v.strip().lower() == "auto"):
+        return -1
+    n = _as_int(v, "watcher.decode_threads")
+    if not 0 <= n <= 64:
+        raise ConfigError(f"watcher.decode_threads must be 'auto' or 0..64, got {v!r}")
+    return n
+
+
 def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
     """Validate the merged dict into :class:`Settings` (raises :class:`ConfigError`)."""
     k = cfg.get("kubernetes") or {}
@@ -349,6 +359,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         list_page_size=max(1, _as_int(w.get("list_page_size", 500), "watcher.list_page_size")),
         watch_interval=_as_float(w.get("watch_interval", 1), "watcher.watch_interval"),
         engine=_choice(w.get("engine", "native"), "watcher.engine", ("native", "python")),
+        decode_threads=_decode_threads(w.get("decode_threads", "auto")),
         state_format=_choice(w.get("state_format", "structured"), "watcher.state_format", ("structured", "python_repr")),
         event_timestamp=_choice(w.get("event_timestamp", "local"), "watcher.event_timestamp", ("local", "utc")),
         log_events=None if w.get("log_events") is None else _as_bool(w.get("log_events"), "watcher.log_events"),

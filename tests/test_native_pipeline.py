@@ -127,3 +127,56 @@ def test_light_parse_defers_payload_subtrees():
     assert ctrl == ["INVALID"]
     assert calls == []
     assert c["events_filtered_critical"] == 1 and "u2" in entries and last_rv == "6"
+
+
+@pytest.mark.parametrize("threads", [0, 1, 4])
+def test_decode_pool_matches_serial(threads):
+    """Phase B (decode) on 0..4 worker threads gives exactly the serial result:
+    same submits in the same order, same cache, same counters, for feeds of
+    every size around the fan-out threshold."""
+    data = stream()
+    lines = data.split(b"\n")[:-1]
+    framed = b"".join(b"%x\r\n%s\r\n" % (len(ln) + 1, ln + b"\n") for ln in lines) + b"0\r\n\r\n"
+    rng = random.Random(threads)
+    cuts, pos = [], 0
+    while pos < len(framed):
+        pos += rng.choice([7, 300, 4000, 20000, 60000])
+        cuts.append(min(pos, len(framed)))
+    pieces = [framed[i:j] for i, j in zip([0] + cuts[:-1], cuts)]
+    ref = run_python("production", {"watcher": {"namespaces": []}}, data)
+    s = load_settings("production", overrides={"watcher": {"namespaces": [], "decode_threads": threads}},
+                      environ={})
+    rec, m = Recorder(), Metrics()
+    p = EventPipeline(s, PyDecoder("production"), rec, m)
+    p.log_events_setting = False
+    p.attach_native()
+    assert p.native.decode_threads() == threads
+    ctrl = []
+    for _ in range(3):  # same stream thrice: the cache sees re-adds of known uids
+        p.native.reset()
+        for piece in pieces:
+            ctrl += p.handle_raw(piece, 0, framed=True)
+    assert rec.calls[:len(ref[0])] == ref[0]
+    assert len(rec.calls) == 3 * len(ref[0])
+    assert norm_cache(p.cache.entries) == norm_cache(ref[1])
+    assert [c[0] for c in ctrl] == ["INVALID", "ERROR"] * 3
+
+
+def test_decode_pool_lifecycle():
+    """Pools are created and joined with their pipelines (no leaked threads)."""
+    import os
+    from k8s_watcher_amd.ops.native import load
+    mod = load()
+
+    def os_threads():
+        return len(os.listdir("/proc/self/task"))
+
+    before = os_threads()
+    for _ in range(20):
+        pl = mod.Pipeline("production", {}, {}, None, True, False, 1, 0, True, True, None, False, False, 3)
+        assert os_threads() == before + 3
+        pl.feed(stream(), 0)
+        del pl
+    assert os_threads() == before
+    with pytest.raises(ValueError):
+        mod.Pipeline("production", {}, {}, None, True, False, 1, 0, True, True, None, False, False, 65)
