@@ -60,6 +60,7 @@ def parse_args(argv=None):
     ap.add_argument("--connections", type=int, default=None, help="notifier pool connections")
     ap.add_argument("--pipeline-depth", type=int, default=None)
     ap.add_argument("--decode-threads", default=None, help="watcher.decode_threads (int or auto)")
+    ap.add_argument("--decode-affinity", default=None, choices=["none", "l3"])
     ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
     ap.add_argument("--sink-workers", type=int, default=4)
     ap.add_argument("--latency-rate", type=float, default=100.0)
@@ -144,7 +145,8 @@ async def rank_main(args, d: Dist) -> dict:
             "clusterapi": {"base_url": f"http://127.0.0.1:{sink_port}", "timeout": 30,
                            "enabled": not os.environ.get("BENCH_NO_NOTIFY")},
             "watcher": {"engine": args.engine, "retry": {"max_attempts": 0, "delay_seconds": 0.05},
-                        **({"decode_threads": args.decode_threads} if args.decode_threads is not None else {})},
+                        **({"decode_threads": args.decode_threads} if args.decode_threads is not None else {}),
+                        **({"decode_affinity": args.decode_affinity} if args.decode_affinity else {})},
         }
         pool = {}
         if args.connections:

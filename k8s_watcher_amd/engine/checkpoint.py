@@ -18,7 +18,7 @@ import os
 import tempfile
 from typing import Dict, Optional, Tuple
 
-from ..ops.cache import PodCache
+from ..ops.cache import PodCache, make_pod_cache
 
 FORMAT_VERSION = 1
 
@@ -44,8 +44,9 @@ def save_checkpoint(path: str, scopes: Dict[str, Optional[str]], cache: PodCache
         raise
 
 
-def load_checkpoint(path: str) -> Optional[Tuple[Dict[str, Optional[str]], PodCache, dict]]:
-    """``(scopes, cache, meta)`` or None when absent/unreadable/incompatible."""
+def load_checkpoint(path: str, native_cache: bool = False) -> Optional[Tuple[Dict[str, Optional[str]], PodCache, dict]]:
+    """``(scopes, cache, meta)`` or None when absent/unreadable/incompatible.
+    ``native_cache`` loads into a ``_kwcore.PodCache`` (native pipeline)."""
     try:
         with open(path, "r", encoding="utf-8") as fh:
             doc = json.load(fh)
@@ -55,4 +56,4 @@ def load_checkpoint(path: str) -> Optional[Tuple[Dict[str, Optional[str]], PodCa
         return None
     if not isinstance(doc, dict) or doc.get("version") != FORMAT_VERSION:
         return None
-    return doc.get("scopes") or {}, PodCache.from_records(doc.get("cache") or []), doc.get("meta") or {}
+    return doc.get("scopes") or {}, make_pod_cache(native_cache, doc.get("cache") or []), doc.get("meta") or {}

@@ -21,7 +21,7 @@ import logging
 from typing import List, Optional
 
 from ..metrics import Metrics
-from ..ops.cache import CORE, MISSING, NAME, NS, PHASE, PodCache
+from ..ops.cache import CORE, MISSING, NAME, NS, PHASE, PodCache, make_pod_cache
 from ..ops.decode import (ADDED, BOOKMARK, DELETED, E_EXTRA, E_HAS_STATUS, E_NAME, E_NS, E_PHASE,
                           E_RV, E_TYPE, E_UID, MODIFIED)
 from ..ops.filters import TERMINAL_PHASES
@@ -75,10 +75,12 @@ class EventPipeline:
         from ..utils.cpus import auto_decode_threads
         w = self.settings.watcher
         core = getattr(self.notifier, "core", None)
+        if isinstance(self.cache, PodCache):  # the fused pipeline keeps the cache in C++
+            self.cache = make_pod_cache(True, self.cache.to_records())
         decode = decode_pool if decode_pool is not None else (
             w.decode_threads if w.decode_threads >= 0 else auto_decode_threads())
         self.native = load().Pipeline(
-            self.settings.environment, self.cache.entries, self.metrics.c, self.namespaces or None,
+            self.settings.environment, self.cache, self.metrics.c, self.namespaces or None,
             self.critical_active, self.phase_mode, self.shard.count, self.shard.index, self.shard.by_uid,
             w.event_timestamp == "utc", core, False, False, decode)
 
@@ -110,7 +112,8 @@ class EventPipeline:
         """Process decoded events; returns control events (ERROR/INVALID) for the reflector."""
         ctrl: List[tuple] = []
         c = self.metrics.c
-        entries = self.cache.entries
+        observe = self.cache.observe
+        set_core = self.cache.set_core
         critical = self.critical_active
         nsset = self.namespaces
         phase_mode = self.phase_mode
@@ -144,18 +147,7 @@ class EventPipeline:
             phase = ev[E_PHASE]
             ns = ev[E_NS]
             name = ev[E_NAME]
-            # cache update (inline PodCache.observe for speed)
-            ent = entries.get(uid)
-            prev = MISSING if ent is None else ent[PHASE]
-            if et == DELETED:
-                if ent is not None:
-                    del entries[uid]
-            elif ent is None:
-                ent = [rv, phase, ns, name, None]
-                entries[uid] = ent
-            else:
-                ent[0] = rv
-                ent[PHASE] = phase
+            prev = observe(et, uid, rv, phase, ns, name)
             if critical and not (et == DELETED or not ev[E_HAS_STATUS] or phase in TERMINAL_PHASES):
                 c["events_filtered_critical"] += 1
                 continue
@@ -173,7 +165,7 @@ class EventPipeline:
             if core is None:
                 core = decoder.core(ev)
             if et != DELETED:
-                ent[CORE] = core
+                set_core(uid, core)
             if ts is None:
                 ts = event_timestamp(self.ts_mode)
             submit(uid, et, ns, name, core, read_ns, ts)
@@ -191,18 +183,18 @@ class EventPipeline:
         ``notify=False`` the cache is primed silently (``initial_list: skip``).
         ``scope_ns`` limits deletions to one namespace (server-side scopes).
         """
-        entries = self.cache.entries
+        cache = self.cache
         out: List[tuple] = []
         seen = set()
         for ev in listed:
             uid = ev[E_UID]
             seen.add(uid)
-            ent = entries.get(uid)
+            ent = cache.get(uid)
             if ent is None:
                 out.append(ev)
             elif ent[0] != ev[E_RV]:
                 out.append((MODIFIED,) + ev[1:])
-        for uid, ent in list(entries.items()):
+        for uid, ent in cache.items():
             if uid in seen or (scope_ns is not None and ent[NS] != scope_ns):
                 continue
             core = ent[CORE]
@@ -215,9 +207,9 @@ class EventPipeline:
                 if self.shard.active and not self.shard.owns(uid, ev[E_NS]):
                     continue
                 if ev[E_TYPE] == DELETED:
-                    entries.pop(uid, None)
+                    cache.pop(uid, None)
                 else:
-                    entries[uid] = [ev[E_RV], ev[E_PHASE], ev[E_NS], ev[E_NAME], None]
+                    cache.put(uid, ev[E_RV], ev[E_PHASE], ev[E_NS], ev[E_NAME], None)
             return []
         saved_rv = self.last_rv
         ctrl = self.handle_batch(out, read_ns)

@@ -32,7 +32,7 @@ from ..kube.api import ApiError, KubeApi
 from ..kube.kubeconfig import ConfigException, KubeEndpoint, load_incluster_config, load_kube_config
 from ..metrics import Metrics, start_metrics_server
 from ..net.http import HttpError
-from ..ops.cache import PodCache
+from ..ops.cache import make_pod_cache
 from ..ops.decode import make_decoder
 from ..parallel.native_notifier import NativeNotifierPool
 from ..parallel.notifier import NotifierPool, NullNotifier
@@ -157,11 +157,11 @@ class WatcherService:
         if s.watcher.shard.count > 1:
             self.log.info(f"Shard {s.watcher.shard.index}/{s.watcher.shard.count} "
                           f"(key={s.watcher.shard.key}); watch scopes: {[x or '*' for x in scopes]}")
-        cache = PodCache()
+        cache = make_pod_cache(self._native_pipeline())
         saved_rvs = {}
         ck = s.watcher.checkpoint.path
         if ck:
-            loaded = load_checkpoint(ck)
+            loaded = load_checkpoint(ck, native_cache=self._native_pipeline())
             if loaded is not None:
                 saved_rvs, cache, _ = loaded
                 self.log.info(f"Resuming from checkpoint {ck}: {len(cache)} cached pods")
@@ -206,9 +206,12 @@ class WatcherService:
     def _make_decode_pool(self):
         """One decode pool for every watch scope (they share the loop thread)."""
         from ..ops.native import load
-        from ..utils.cpus import auto_decode_threads
+        from ..utils.cpus import auto_decode_threads, pin_to_l3_domain
         w = self.settings.watcher
         n = w.decode_threads if w.decode_threads >= 0 else auto_decode_threads()
+        if n > 0 and w.decode_affinity == "l3":
+            dom = pin_to_l3_domain()  # workers started below inherit the mask
+            self.log.info(f"Decode pool pinned to L3 domain CPUs {sorted(dom) if dom else 'unavailable'}")
         return load().DecodePool(n) if n > 0 else 0
 
     def _native_pipeline(self) -> bool:

@@ -10,6 +10,12 @@ reflector turn a post-410 relist into exact ADDED/MODIFIED/DELETED diffs
 One entry per live pod: ``uid -> [resourceVersion, phase, namespace, name, core]``
 where ``core`` is the last serialized payload core (or ``None`` if the pod
 was never notified).
+
+Two implementations share this interface: :class:`PodCache` (a dict of
+lists, used by the Python engine) and ``_kwcore.PodCache`` (C++,
+``ops/csrc/podcache.inc``), which the fused native pipeline updates without
+creating Python objects. Callers other than the two pipelines use only the
+methods below; ``get``/``items``/``pop`` of the native cache return copies.
 """
 
 from __future__ import annotations
@@ -55,20 +61,45 @@ class PodCache:
         if ent is not None:
             ent[CORE] = core
 
-    def items(self) -> Iterator[Tuple[str, list]]:
-        return iter(self.entries.items())
+    def put(self, uid: str, rv: Optional[str], phase: Optional[str], ns: Optional[str],
+            name: Optional[str], core: Optional[bytes] = None) -> None:
+        self.entries[uid] = [rv, phase, ns, name, core]
+
+    def pop(self, uid: str, default=None):
+        return self.entries.pop(uid, default)
+
+    def clear(self) -> None:
+        self.entries.clear()
+
+    def items(self) -> List[Tuple[str, list]]:
+        return list(self.entries.items())
 
     def to_records(self) -> List[list]:
         return [[uid] + ent[:4] + [ent[CORE].decode("utf-8") if ent[CORE] else None]
                 for uid, ent in self.entries.items()]
 
+    def load_records(self, records: List[list]) -> None:
+        for r in records:
+            uid, rv, phase, ns, name, core = r
+            self.entries[uid] = [rv, phase, ns, name, core.encode("utf-8") if core else None]
+
     @classmethod
     def from_records(cls, records: List[list]) -> "PodCache":
         c = cls()
-        for r in records:
-            uid, rv, phase, ns, name, core = r
-            c.entries[uid] = [rv, phase, ns, name, core.encode("utf-8") if core else None]
+        c.load_records(records)
         return c
+
+
+def make_pod_cache(native: bool, records: Optional[List[list]] = None):
+    """A :class:`PodCache` or, for the native pipeline, a ``_kwcore.PodCache``."""
+    if native:
+        from .native import load
+        cache = load().PodCache(MISSING)
+    else:
+        cache = PodCache()
+    if records:
+        cache.load_records(records)
+    return cache
 
 
 def phase_changed(etype: str, prev, phase: Optional[str]) -> bool:

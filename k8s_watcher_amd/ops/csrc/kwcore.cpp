@@ -32,6 +32,7 @@
 #include <cstring>
 #include <ctime>
 #include <deque>
+#include <memory>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -1758,6 +1759,7 @@ PyObject* kw_bench_parse(PyObject*, PyObject* args) {
     return Py_BuildValue("(dn)", secs, (Py_ssize_t)sink);
 }
 
+#include "podcache.inc"
 #include "engine.inc"
 
 PyMethodDef module_methods[] = {
@@ -1795,7 +1797,7 @@ PyMODINIT_FUNC PyInit__kwcore(void) {
     if (PyType_Ready(&ScannerType) < 0) return nullptr;
     Py_INCREF(&ScannerType);
     PyModule_AddObject(m, "ResponseScanner", (PyObject*)&ScannerType);
-    if (register_engine(m) < 0 || register_pipeline(m) < 0) return nullptr;
+    if (register_engine(m) < 0 || register_podcache(m) < 0 || register_pipeline(m) < 0) return nullptr;
     const char* names[6] = {"ADDED", "MODIFIED", "DELETED", "BOOKMARK", "ERROR", "INVALID"};
     for (int i = 0; i < 6; ++i) {
         g_types[i] = PyUnicode_InternFromString(names[i]);

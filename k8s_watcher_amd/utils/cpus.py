@@ -56,3 +56,60 @@ def auto_decode_threads(cpus: Optional[int] = None) -> int:
     apply phase caps the gain beyond ~4-way decode)."""
     cpus = available_cpus() if cpus is None else cpus
     return max(0, min(3, cpus - 2))
+
+
+def _parse_cpu_list(text: str) -> set:
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.update(range(int(a), int(b) + 1))
+        else:
+            cpus.add(int(part))
+    return cpus
+
+
+def current_cpu() -> Optional[int]:
+    """CPU the calling thread last ran on (field 39 of /proc/thread-self/stat)."""
+    try:
+        with open("/proc/thread-self/stat") as fh:
+            stat = fh.read()
+        return int(stat[stat.rindex(")") + 2:].split()[36])
+    except (OSError, ValueError, IndexError):
+        return None
+
+
+def l3_domain_cpus(cpu: Optional[int] = None, root: str = "") -> Optional[set]:
+    """Allowed CPUs sharing the last-level cache with ``cpu`` (default: the
+    CPU this thread runs on). On chiplet CPUs (one L3 per CCD) keeping the
+    event-loop thread and its decode workers inside one L3 keeps the watch
+    bytes and decoded spans from crossing the fabric twice per event."""
+    if cpu is None:
+        cpu = current_cpu()
+        if cpu is None:
+            return None
+    try:
+        with open(f"{root}/sys/devices/system/cpu/cpu{cpu}/cache/index3/shared_cpu_list") as fh:
+            dom = _parse_cpu_list(fh.read())
+    except (OSError, ValueError):
+        return None
+    try:
+        dom &= os.sched_getaffinity(0)
+    except (AttributeError, OSError):
+        pass
+    return dom or None
+
+
+def pin_to_l3_domain() -> Optional[set]:
+    """Restrict the calling thread (and threads it starts later, which inherit
+    the mask) to its current L3 domain; returns the CPU set or None."""
+    dom = l3_domain_cpus()
+    if not dom:
+        return None
+    try:
+        os.sched_setaffinity(0, dom)
+    except OSError:
+        return None
+    return dom

@@ -52,7 +52,7 @@ def run_python(env, ov, data):
     p = EventPipeline(s, PyDecoder(env), rec, m)
     p.log_events_setting = False
     ctrl = p.handle_batch(PyDecoder(env).feed(data), 0)
-    return rec.calls, p.cache.entries, m.c, p.last_rv, [c[0] for c in ctrl]
+    return rec.calls, p.cache, m.c, p.last_rv, [c[0] for c in ctrl]
 
 
 def run_native(env, ov, data, framed_chunks=None):
@@ -67,11 +67,11 @@ def run_native(env, ov, data, framed_chunks=None):
     else:
         for piece in framed_chunks:
             ctrl += p.handle_raw(piece, 0, framed=True)
-    return rec.calls, p.cache.entries, m.c, p.last_rv, [c[0] for c in ctrl]
+    return rec.calls, p.cache, m.c, p.last_rv, [c[0] for c in ctrl]
 
 
-def norm_cache(entries):
-    return {u: [e[0], e[1], e[2], e[3], json.loads(e[4]) if e[4] else None] for u, e in entries.items()}
+def norm_cache(cache):
+    return {u: [e[0], e[1], e[2], e[3], json.loads(e[4]) if e[4] else None] for u, e in cache.items()}
 
 
 @pytest.mark.parametrize("env,ov", PROFILES)
@@ -158,7 +158,7 @@ def test_decode_pool_matches_serial(threads):
             ctrl += p.handle_raw(piece, 0, framed=True)
     assert rec.calls[:len(ref[0])] == ref[0]
     assert len(rec.calls) == 3 * len(ref[0])
-    assert norm_cache(p.cache.entries) == norm_cache(ref[1])
+    assert norm_cache(p.cache) == norm_cache(ref[1])
     assert [c[0] for c in ctrl] == ["INVALID", "ERROR"] * 3
 
 
@@ -173,10 +173,10 @@ def test_decode_pool_lifecycle():
 
     before = os_threads()
     for _ in range(20):
-        pl = mod.Pipeline("production", {}, {}, None, True, False, 1, 0, True, True, None, False, False, 3)
+        pl = mod.Pipeline("production", mod.PodCache(), {}, None, True, False, 1, 0, True, True, None, False, False, 3)
         assert os_threads() == before + 3
         pl.feed(stream(), 0)
         del pl
     assert os_threads() == before
     with pytest.raises(ValueError):
-        mod.Pipeline("production", {}, {}, None, True, False, 1, 0, True, True, None, False, False, 65)
+        mod.Pipeline("production", mod.PodCache(), {}, None, True, False, 1, 0, True, True, None, False, False, 65)
