@@ -60,7 +60,7 @@ def parse_args(argv=None):
     ap.add_argument("--connections", type=int, default=None, help="notifier pool connections")
     ap.add_argument("--pipeline-depth", type=int, default=None)
     ap.add_argument("--decode-threads", default=None, help="watcher.decode_threads (int or auto)")
-    ap.add_argument("--decode-affinity", default=None, choices=["none", "l3"])
+    ap.add_argument("--decode-affinity", default=None, choices=["auto", "none", "l3"])
     ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
     ap.add_argument("--sink-workers", type=int, default=4)
     ap.add_argument("--latency-rate", type=float, default=100.0)

@@ -209,9 +209,14 @@ class WatcherService:
         from ..utils.cpus import auto_decode_threads, pin_to_l3_domain
         w = self.settings.watcher
         n = w.decode_threads if w.decode_threads >= 0 else auto_decode_threads()
-        if n > 0 and w.decode_affinity == "l3":
-            dom = pin_to_l3_domain()  # workers started below inherit the mask
-            self.log.info(f"Decode pool pinned to L3 domain CPUs {sorted(dom) if dom else 'unavailable'}")
+        if n > 0 and w.decode_affinity != "none":
+            # Workers started below inherit the mask. Measured on a chiplet
+            # host (BENCHMARKS.md): 3 workers spread over CCDs were slower than
+            # none; the same 3 inside the loop thread's L3 ran ~1.6x faster.
+            auto = w.decode_affinity == "auto"
+            dom = pin_to_l3_domain(min_cpus=n + 1 if auto else 1, only_if_split=auto)
+            if dom:
+                self.log.info(f"Decode pool pinned to L3 domain CPUs {sorted(dom)}")
         return load().DecodePool(n) if n > 0 else 0
 
     def _native_pipeline(self) -> bool:

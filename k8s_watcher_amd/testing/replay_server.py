@@ -36,6 +36,7 @@ from __future__ import annotations
 import argparse
 import asyncio
 import json
+import os
 import re
 import sys
 import time
@@ -133,9 +134,21 @@ class ReplayServer:
         self.live: Dict[str, Tuple[int, int]] = {}
         if template.kind == "steady":
             self.live = {uid: (-1, j) for j, (_, uid) in enumerate(template.initial)}
-        # Whole steps rendered ahead of time so that, during a timed step, this
-        # process only issues send() calls and can never be the bottleneck.
-        self.rendered = {k: self.t.render(k, 0, self.E) for k in range(prerender)}
+        # Whole steps rendered ahead of time into memory files so that, during
+        # a timed step, this process only issues sendfile() calls: the kernel
+        # moves the bytes (no user-space copy), which keeps this fixture well
+        # ahead of the watcher it feeds.
+        self.rendered = {k: self._to_memfile(*self.t.render(k, 0, self.E)) for k in range(prerender)}
+
+    @staticmethod
+    def _to_memfile(data: bytes, offsets: List[int]):
+        if not hasattr(os, "memfd_create"):
+            return data, offsets
+        fd = os.memfd_create("replay-step")
+        view = memoryview(data)
+        while view:
+            view = view[os.write(fd, view):]
+        return open(fd, "rb"), offsets
 
     # ------------------------------------------------------------------ state
     def pos_of(self, rv: int) -> Tuple[int, int]:
@@ -291,6 +304,11 @@ class ReplayServer:
             data, offsets = pre
         else:
             data, offsets = self.t.render(step, 0, n)
+        if not isinstance(data, bytes):  # a prerendered memory file
+            try:
+                return await self._send_file(step, n, data, offsets, drop_at, expire_at)
+            finally:
+                data.close()
         offsets = offsets + [len(data)]
         view = memoryview(data)
         i = 0
@@ -302,6 +320,40 @@ class ReplayServer:
             # that joins while we wait for drains gets exactly the events after this slice
             self._advance(step, i, j)
             await self._broadcast(view[offsets[i]:offsets[j]])
+            i = j
+            if cut is not None and i == cut:
+                if drop_at is not None:
+                    self.drop()
+                else:
+                    self.expire()
+                cut = None
+                await asyncio.sleep(0)
+        return n
+
+
+    async def _send_file(self, step: int, n: int, f, offsets: List[int], drop_at: Optional[int],
+                         expire_at: Optional[int]) -> int:
+        """``send`` for a prerendered step: same slicing, drop/expire points and
+        watcher bookkeeping, but each slice goes out with sendfile()."""
+        loop = asyncio.get_running_loop()
+        size = os.fstat(f.fileno()).st_size
+        offsets = offsets + [size]
+        cut = drop_at if drop_at is not None else expire_at
+        i = 0
+        while i < n:
+            j = min(n, i + 1024)
+            if cut is not None and i < cut <= j:
+                j = cut
+            # advance before the first await (as _broadcast): a watch that joins
+            # while this slice is in flight gets it from its backlog instead
+            self._advance(step, i, j)
+            targets = list(self.watchers)
+            if targets:
+                res = await asyncio.gather(*(loop.sendfile(w.transport, f, offsets[i], offsets[j] - offsets[i])
+                                             for w in targets), return_exceptions=True)
+                for w, r in zip(targets, res):
+                    if isinstance(r, BaseException) and not isinstance(r, (ConnectionError, RuntimeError)):
+                        raise r
             i = j
             if cut is not None and i == cut:
                 if drop_at is not None:

@@ -102,12 +102,22 @@ def l3_domain_cpus(cpu: Optional[int] = None, root: str = "") -> Optional[set]:
     return dom or None
 
 
-def pin_to_l3_domain() -> Optional[set]:
+def pin_to_l3_domain(min_cpus: int = 1, only_if_split: bool = False) -> Optional[set]:
     """Restrict the calling thread (and threads it starts later, which inherit
-    the mask) to its current L3 domain; returns the CPU set or None."""
+    the mask) to its current L3 domain; returns the CPU set or None.
+
+    ``min_cpus``: leave the mask alone if the domain has fewer usable CPUs.
+    ``only_if_split``: only pin when the allowed CPUs span several L3 domains
+    (on a single-L3 machine pinning buys nothing)."""
     dom = l3_domain_cpus()
-    if not dom:
+    if not dom or len(dom) < min_cpus:
         return None
+    if only_if_split:
+        try:
+            if dom >= os.sched_getaffinity(0):
+                return None
+        except (AttributeError, OSError):
+            return None
     try:
         os.sched_setaffinity(0, dom)
     except OSError:
