@@ -61,6 +61,8 @@ def parse_args(argv=None):
     ap.add_argument("--pipeline-depth", type=int, default=None)
     ap.add_argument("--decode-threads", default=None, help="watcher.decode_threads (int or auto)")
     ap.add_argument("--decode-affinity", default=None, choices=["auto", "none", "l3"])
+    ap.add_argument("--no-placement", dest="placement", action="store_false",
+                    help="do not give the watcher and its fixtures separate L3 domains")
     ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
     ap.add_argument("--sink-workers", type=int, default=4)
     ap.add_argument("--latency-rate", type=float, default=100.0)
@@ -83,6 +85,7 @@ class Dist:
 
     def __init__(self) -> None:
         self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank)))
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.pg = None
         if self.world > 1:
@@ -107,10 +110,23 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-async def spawn(*cmd: str):
+async def spawn(*cmd: str, cpus=None):
+    pin = (lambda: os.sched_setaffinity(0, cpus)) if cpus else None
     return await asyncio.create_subprocess_exec(
         *cmd, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
-        stderr=asyncio.subprocess.DEVNULL, start_new_session=True, cwd=ROOT)
+        stderr=asyncio.subprocess.DEVNULL, start_new_session=True, cwd=ROOT, preexec_fn=pin)
+
+
+def placement(local_rank: int):
+    """(watcher L3 domain index, fixture CPU set) for this rank: on a chiplet
+    host each rank's watcher gets its own L3 domain and its replay/sink
+    fixtures the next one, so ranks and fixtures never share a chiplet (as
+    separate watcher pods on separate nodes would not); None/None elsewhere."""
+    from k8s_watcher_amd.utils.cpus import l3_domains
+    doms = l3_domains()
+    if len(doms) < 2:
+        return None, None
+    return (2 * local_rank) % len(doms), set(doms[(2 * local_rank + 1) % len(doms)])
 
 
 async def rank_main(args, d: Dist) -> dict:
@@ -120,12 +136,13 @@ async def rank_main(args, d: Dist) -> dict:
     from k8s_watcher_amd.utils.config import load_settings
     from k8s_watcher_amd.utils.logsetup import setup_logging
 
+    watcher_dom, fixture_cpus = placement(d.local_rank) if args.placement else (None, None)
     replay = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.replay_server",
                          "--pods-per-step", str(args.pods_per_step), "--seed", str(d.rank),
-                         "--prerender", str(args.warmup + args.steps))
+                         "--prerender", str(args.warmup + args.steps), cpus=fixture_cpus)
     sink_port = free_port()
     sink = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.stub_sink", "--port", str(sink_port),
-                       "--workers", str(args.sink_workers))
+                       "--workers", str(args.sink_workers), cpus=fixture_cpus)
     try:
         ready = (await asyncio.wait_for(replay.stdout.readline(), 600)).decode().split()
         assert ready and ready[0] == "READY", ready
@@ -146,7 +163,8 @@ async def rank_main(args, d: Dist) -> dict:
                            "enabled": not os.environ.get("BENCH_NO_NOTIFY")},
             "watcher": {"engine": args.engine, "retry": {"max_attempts": 0, "delay_seconds": 0.05},
                         **({"decode_threads": args.decode_threads} if args.decode_threads is not None else {}),
-                        **({"decode_affinity": args.decode_affinity} if args.decode_affinity else {})},
+                        **({"decode_affinity": args.decode_affinity} if args.decode_affinity else {}),
+                        **({"decode_l3_domain": watcher_dom} if watcher_dom is not None else {})},
         }
         pool = {}
         if args.connections:

@@ -214,7 +214,8 @@ class WatcherService:
             # host (BENCHMARKS.md): 3 workers spread over CCDs were slower than
             # none; the same 3 inside the loop thread's L3 ran ~1.6x faster.
             auto = w.decode_affinity == "auto"
-            dom = pin_to_l3_domain(min_cpus=n + 1 if auto else 1, only_if_split=auto)
+            dom = pin_to_l3_domain(min_cpus=n + 1 if auto else 1, only_if_split=auto,
+                                   index=w.decode_l3_domain)
             if dom:
                 self.log.info(f"Decode pool pinned to L3 domain CPUs {sorted(dom)}")
         return load().DecodePool(n) if n > 0 else 0

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import math
 import os
-from typing import Optional
+from typing import List, Optional
 
 _CGROUP_FILES = ("/sys/fs/cgroup/cpu.max",                      # cgroup v2
                  "/sys/fs/cgroup/cpu/cpu.cfs_quota_us")         # cgroup v1
@@ -102,14 +102,40 @@ def l3_domain_cpus(cpu: Optional[int] = None, root: str = "") -> Optional[set]:
     return dom or None
 
 
-def pin_to_l3_domain(min_cpus: int = 1, only_if_split: bool = False) -> Optional[set]:
-    """Restrict the calling thread (and threads it starts later, which inherit
-    the mask) to its current L3 domain; returns the CPU set or None.
+def l3_domains(root: str = "") -> List[frozenset]:
+    """The allowed CPUs grouped by shared L3, ordered by lowest CPU number."""
+    try:
+        allowed = os.sched_getaffinity(0)
+    except (AttributeError, OSError):
+        return []
+    doms = set()
+    todo = set(allowed)
+    while todo:
+        cpu = min(todo)
+        try:
+            with open(f"{root}/sys/devices/system/cpu/cpu{cpu}/cache/index3/shared_cpu_list") as fh:
+                dom = frozenset(_parse_cpu_list(fh.read()) & allowed) or frozenset([cpu])
+        except (OSError, ValueError):
+            dom = frozenset([cpu])
+        doms.add(dom)
+        todo -= dom | {cpu}
+    return sorted(doms, key=min)
 
-    ``min_cpus``: leave the mask alone if the domain has fewer usable CPUs.
-    ``only_if_split``: only pin when the allowed CPUs span several L3 domains
-    (on a single-L3 machine pinning buys nothing)."""
-    dom = l3_domain_cpus()
+
+def pin_to_l3_domain(min_cpus: int = 1, only_if_split: bool = False, index: Optional[int] = None) -> Optional[set]:
+    """Restrict the calling thread (and threads it starts later, which inherit
+    the mask) to one L3 domain; returns the CPU set or None.
+
+    ``index``: that domain of :func:`l3_domains` (modulo their number) instead
+    of the one the thread runs on — a launcher gives each watcher process its
+    own chiplet this way. ``min_cpus``: leave the mask alone if the domain has
+    fewer usable CPUs. ``only_if_split``: only pin when the allowed CPUs span
+    several L3 domains (on a single-L3 machine pinning buys nothing)."""
+    if index is not None and index >= 0:
+        doms = l3_domains()
+        dom = set(doms[index % len(doms)]) if doms else None
+    else:
+        dom = l3_domains_current()
     if not dom or len(dom) < min_cpus:
         return None
     if only_if_split:
@@ -123,3 +149,7 @@ def pin_to_l3_domain(min_cpus: int = 1, only_if_split: bool = False) -> Optional
     except OSError:
         return None
     return dom
+
+
+def l3_domains_current() -> Optional[set]:
+    return l3_domain_cpus()
