@@ -118,15 +118,21 @@ async def spawn(*cmd: str, cpus=None):
 
 
 def placement(local_rank: int):
-    """(watcher L3 domain index, fixture CPU set) for this rank: on a chiplet
-    host each rank's watcher gets its own L3 domain and its replay/sink
-    fixtures the next one, so ranks and fixtures never share a chiplet (as
-    separate watcher pods on separate nodes would not); None/None elsewhere."""
+    """(watcher L3 domain index, replay CPUs, sink CPUs) for this rank on a
+    chiplet host; all None elsewhere.
+
+    Each rank gets two L3 domains of its own. The replay API server shares the
+    watcher's: on loopback the receiver copies every watch byte out of the
+    sender's socket buffers, and from a remote chiplet that copy crosses the
+    fabric (measured: ~480k vs ~720-830k ev/s) — co-locating them stands in
+    for a NIC that delivers into the consumer's cache. The clusterapi stub
+    (a fifth of the events, small bodies) goes to the second domain."""
     from k8s_watcher_amd.utils.cpus import l3_domains
     doms = l3_domains()
     if len(doms) < 2:
-        return None, None
-    return (2 * local_rank) % len(doms), set(doms[(2 * local_rank + 1) % len(doms)])
+        return None, None, None
+    w = (2 * local_rank) % len(doms)
+    return w, set(doms[w]), set(doms[(2 * local_rank + 1) % len(doms)])
 
 
 async def rank_main(args, d: Dist) -> dict:
@@ -136,13 +142,13 @@ async def rank_main(args, d: Dist) -> dict:
     from k8s_watcher_amd.utils.config import load_settings
     from k8s_watcher_amd.utils.logsetup import setup_logging
 
-    watcher_dom, fixture_cpus = placement(d.local_rank) if args.placement else (None, None)
+    watcher_dom, replay_cpus, sink_cpus = placement(d.local_rank) if args.placement else (None, None, None)
     replay = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.replay_server",
                          "--pods-per-step", str(args.pods_per_step), "--seed", str(d.rank),
-                         "--prerender", str(args.warmup + args.steps), cpus=fixture_cpus)
+                         "--prerender", str(args.warmup + args.steps), cpus=replay_cpus)
     sink_port = free_port()
     sink = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.stub_sink", "--port", str(sink_port),
-                       "--workers", str(args.sink_workers), cpus=fixture_cpus)
+                       "--workers", str(args.sink_workers), cpus=sink_cpus)
     try:
         ready = (await asyncio.wait_for(replay.stdout.readline(), 600)).decode().split()
         assert ready and ready[0] == "READY", ready
