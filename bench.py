@@ -97,6 +97,13 @@ class Dist:
         if self.world > 1:
             self.dist.barrier()
 
+    def broadcast(self, obj):
+        if self.world == 1:
+            return obj
+        box = [obj]
+        self.dist.broadcast_object_list(box, src=0)
+        return box[0]
+
     def reduce(self, value: float, op: str) -> float:
         if self.world == 1:
             return value
@@ -117,22 +124,37 @@ async def spawn(*cmd: str, cpus=None):
         stderr=asyncio.subprocess.DEVNULL, start_new_session=True, cwd=ROOT, preexec_fn=pin)
 
 
-def placement(local_rank: int):
-    """(watcher L3 domain index, replay CPUs, sink CPUs) for this rank on a
+def cpu_ranges(cpus) -> "str | None":
+    if not cpus:
+        return None
+    out, run = [], []
+    for c in sorted(cpus):
+        if run and c != run[-1] + 1:
+            out.append(f"{run[0]}-{run[-1]}" if len(run) > 1 else str(run[0]))
+            run = []
+        run.append(c)
+    out.append(f"{run[0]}-{run[-1]}" if len(run) > 1 else str(run[0]))
+    return ",".join(out)
+
+
+def placement(d: "Dist"):
+    """(watcher L3 domain CPUs, replay CPUs, sink CPUs) for this rank on a
     chiplet host; all None elsewhere.
 
-    Each rank gets two L3 domains of its own. The replay API server shares the
-    watcher's: on loopback the receiver copies every watch byte out of the
-    sender's socket buffers, and from a remote chiplet that copy crosses the
-    fabric (measured: ~480k vs ~720-830k ev/s) — co-locating them stands in
-    for a NIC that delivers into the consumer's cache. The clusterapi stub
-    (a fifth of the events, small bodies) goes to the second domain."""
-    from k8s_watcher_amd.utils.cpus import l3_domains
-    doms = l3_domains()
-    if len(doms) < 2:
+    Each rank gets two L3 domains of its own, taken from the most idle ones
+    (rank 0 samples /proc/stat and broadcasts the order, so ranks never
+    share). The replay API server shares the watcher's domain: on loopback
+    the receiver copies every watch byte out of the sender's socket buffers,
+    and from a remote chiplet that copy crosses the fabric — co-locating them
+    stands in for a NIC that delivers into the consumer's cache. The
+    clusterapi stub (a fifth of the events, small bodies) gets the second."""
+    from k8s_watcher_amd.utils.cpus import l3_domains_by_idle
+    doms = [sorted(x) for x in l3_domains_by_idle()] if d.rank == 0 else None
+    doms = d.broadcast(doms)
+    if not doms or len(doms) < 2:
         return None, None, None
-    w = (2 * local_rank) % len(doms)
-    return w, set(doms[w]), set(doms[(2 * local_rank + 1) % len(doms)])
+    w = set(doms[(2 * d.local_rank) % len(doms)])
+    return w, w, set(doms[(2 * d.local_rank + 1) % len(doms)])
 
 
 async def rank_main(args, d: Dist) -> dict:
@@ -142,7 +164,9 @@ async def rank_main(args, d: Dist) -> dict:
     from k8s_watcher_amd.utils.config import load_settings
     from k8s_watcher_amd.utils.logsetup import setup_logging
 
-    watcher_dom, replay_cpus, sink_cpus = placement(d.local_rank) if args.placement else (None, None, None)
+    watcher_cpus, replay_cpus, sink_cpus = placement(d) if args.placement else (None, None, None)
+    if watcher_cpus:
+        os.sched_setaffinity(0, watcher_cpus)
     replay = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.replay_server",
                          "--pods-per-step", str(args.pods_per_step), "--seed", str(d.rank),
                          "--prerender", str(args.warmup + args.steps), cpus=replay_cpus)
@@ -169,8 +193,8 @@ async def rank_main(args, d: Dist) -> dict:
                            "enabled": not os.environ.get("BENCH_NO_NOTIFY")},
             "watcher": {"engine": args.engine, "retry": {"max_attempts": 0, "delay_seconds": 0.05},
                         **({"decode_threads": args.decode_threads} if args.decode_threads is not None else {}),
-                        **({"decode_affinity": args.decode_affinity} if args.decode_affinity else {}),
-                        **({"decode_l3_domain": watcher_dom} if watcher_dom is not None else {})},
+                        # placement already pinned this thread (the decode workers inherit it)
+                        **({"decode_affinity": args.decode_affinity or ("none" if watcher_cpus else "auto")})},
         }
         pool = {}
         if args.connections:
@@ -254,7 +278,8 @@ async def rank_main(args, d: Dist) -> dict:
                 "p50_ns": p50, "p99_ns": p99, "lat_samples": lat_n, "sat_p50_ns": sat_p50,
                 "failed": failed, "ref": ref,
                 "cpu_util": {k: round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0},
-                "decode_threads": decode_threads}
+                "decode_threads": decode_threads,
+                "placement": {"watcher_replay": cpu_ranges(watcher_cpus), "sink": cpu_ranges(sink_cpus)}}
     finally:
         for p in (replay, sink):
             try:
@@ -378,6 +403,7 @@ def main(argv=None) -> int:
         "notified_per_s": round(notified / elapsed, 1),
         "notify_failed": res["failed"],
         "cpu_util_rank0": res["cpu_util"],
+        "placement_rank0": res["placement"],
         "saturated_p50_latency_ms": round(res["sat_p50_ns"] / 1e6, 3) if res["sat_p50_ns"] else None,
         "reference_equiv": ({"events_per_s": round(ref_rate, 1), "events": ref["events"],
                              "notified": ref["notified"],

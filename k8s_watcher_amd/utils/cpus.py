@@ -153,3 +153,40 @@ def pin_to_l3_domain(min_cpus: int = 1, only_if_split: bool = False, index: Opti
 
 def l3_domains_current() -> Optional[set]:
     return l3_domain_cpus()
+
+
+def _cpu_times() -> dict:
+    """cpu -> (idle+iowait jiffies, total jiffies) from /proc/stat."""
+    out = {}
+    with open("/proc/stat") as fh:
+        for line in fh:
+            if not line.startswith("cpu") or line.startswith("cpu "):
+                continue
+            f = line.split()
+            vals = [int(x) for x in f[1:]]
+            out[int(f[0][3:])] = (vals[3] + (vals[4] if len(vals) > 4 else 0), sum(vals[:8]))
+    return out
+
+
+def l3_domains_by_idle(sample_s: float = 0.25) -> List[frozenset]:
+    """:func:`l3_domains`, most idle first (idle CPU time summed over a short
+    sample). On a shared host a fixed choice can land on a chiplet that other
+    tenants or interrupt handling keep busy."""
+    import time
+    doms = l3_domains()
+    try:
+        a = _cpu_times()
+        time.sleep(sample_s)
+        b = _cpu_times()
+    except (OSError, ValueError):
+        return doms
+
+    def idle(dom) -> float:
+        tot = 0.0
+        for c in dom:
+            if c in a and c in b:
+                di, dt = b[c][0] - a[c][0], b[c][1] - a[c][1]
+                tot += di / dt if dt > 0 else 1.0
+        return tot
+
+    return sorted(doms, key=lambda d: (-idle(d), min(d)))
