@@ -62,7 +62,7 @@ def parse_args(argv=None):
     ap.add_argument("--decode-threads", default=None, help="watcher.decode_threads (int or auto)")
     ap.add_argument("--decode-affinity", default=None, choices=["auto", "none", "l3"])
     ap.add_argument("--no-placement", dest="placement", action="store_false",
-                    help="do not give the watcher and its fixtures separate L3 domains")
+                    help="no per-rank L3 domain assignment (each watcher still pins per watcher.decode_affinity)")
     ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
     ap.add_argument("--sink-workers", type=int, default=4)
     ap.add_argument("--latency-rate", type=float, default=100.0)
@@ -97,12 +97,12 @@ class Dist:
         if self.world > 1:
             self.dist.barrier()
 
-    def broadcast(self, obj):
+    def all_gather(self, obj) -> list:
         if self.world == 1:
-            return obj
-        box = [obj]
-        self.dist.broadcast_object_list(box, src=0)
-        return box[0]
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
 
     def reduce(self, value: float, op: str) -> float:
         if self.world == 1:
@@ -117,11 +117,10 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-async def spawn(*cmd: str, cpus=None):
-    pin = (lambda: os.sched_setaffinity(0, cpus)) if cpus else None
+async def spawn(*cmd: str):
     return await asyncio.create_subprocess_exec(
         *cmd, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
-        stderr=asyncio.subprocess.DEVNULL, start_new_session=True, cwd=ROOT, preexec_fn=pin)
+        stderr=asyncio.subprocess.DEVNULL, start_new_session=True, cwd=ROOT)
 
 
 def cpu_ranges(cpus) -> "str | None":
@@ -138,23 +137,21 @@ def cpu_ranges(cpus) -> "str | None":
 
 
 def placement(d: "Dist"):
-    """(watcher L3 domain CPUs, replay CPUs, sink CPUs) for this rank on a
-    chiplet host; all None elsewhere.
+    """L3 domain for this rank's watcher on a chiplet host (None elsewhere).
 
-    Each rank gets two L3 domains of its own, taken from the most idle ones
-    (rank 0 samples /proc/stat and broadcasts the order, so ranks never
-    share). The replay API server shares the watcher's domain: on loopback
-    the receiver copies every watch byte out of the sender's socket buffers,
-    and from a remote chiplet that copy crosses the fabric — co-locating them
-    stands in for a NIC that delivers into the consumer's cache. The
-    clusterapi stub (a fifth of the events, small bodies) gets the second."""
-    from k8s_watcher_amd.utils.cpus import l3_domains_by_idle
-    doms = [sorted(x) for x in l3_domains_by_idle()] if d.rank == 0 else None
-    doms = d.broadcast(doms)
-    if not doms or len(doms) < 2:
-        return None, None, None
-    w = set(doms[(2 * d.local_rank) % len(doms)])
-    return w, w, set(doms[(2 * d.local_rank + 1) % len(doms)])
+    Every rank keeps the domain it is already running on — its memory is
+    local there; measured on the MI355X host, moving the watcher and its
+    fixtures to other chiplets after start-up cost ~30% — unless a lower rank
+    holds it, in which case it takes a free domain on the same socket.
+    The replay and sink fixtures are not pinned."""
+    from k8s_watcher_amd.utils.cpus import assign_domains, l3_domain_cpus, l3_domains
+    doms = l3_domains()
+    if len(doms) < 2:
+        return None
+    cur = l3_domain_cpus()
+    here = next((i for i, x in enumerate(doms) if cur and x == frozenset(cur)), 0)
+    wanted = d.all_gather(here)
+    return set(doms[assign_domains(wanted, doms)[d.rank]])
 
 
 async def rank_main(args, d: Dist) -> dict:
@@ -164,15 +161,15 @@ async def rank_main(args, d: Dist) -> dict:
     from k8s_watcher_amd.utils.config import load_settings
     from k8s_watcher_amd.utils.logsetup import setup_logging
 
-    watcher_cpus, replay_cpus, sink_cpus = placement(d) if args.placement else (None, None, None)
+    watcher_cpus = placement(d) if args.placement else None
     if watcher_cpus:
-        os.sched_setaffinity(0, watcher_cpus)
+        os.sched_setaffinity(0, watcher_cpus)  # the decode workers inherit it
     replay = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.replay_server",
                          "--pods-per-step", str(args.pods_per_step), "--seed", str(d.rank),
-                         "--prerender", str(args.warmup + args.steps), cpus=replay_cpus)
+                         "--prerender", str(args.warmup + args.steps))
     sink_port = free_port()
     sink = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.stub_sink", "--port", str(sink_port),
-                       "--workers", str(args.sink_workers), cpus=sink_cpus)
+                       "--workers", str(args.sink_workers))
     try:
         ready = (await asyncio.wait_for(replay.stdout.readline(), 600)).decode().split()
         assert ready and ready[0] == "READY", ready
@@ -279,7 +276,7 @@ async def rank_main(args, d: Dist) -> dict:
                 "failed": failed, "ref": ref,
                 "cpu_util": {k: round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0},
                 "decode_threads": decode_threads,
-                "placement": {"watcher_replay": cpu_ranges(watcher_cpus), "sink": cpu_ranges(sink_cpus)}}
+                "placement": {"watcher": cpu_ranges(watcher_cpus)}}
     finally:
         for p in (replay, sink):
             try:

@@ -190,3 +190,29 @@ def l3_domains_by_idle(sample_s: float = 0.25) -> List[frozenset]:
         return tot
 
     return sorted(doms, key=lambda d: (-idle(d), min(d)))
+
+
+def package_of(cpu: int, root: str = "") -> int:
+    try:
+        with open(f"{root}/sys/devices/system/cpu/cpu{cpu}/topology/physical_package_id") as fh:
+            return int(fh.read().strip())
+    except (OSError, ValueError):
+        return 0
+
+
+def assign_domains(wanted: List[int], doms: List[frozenset]) -> List[int]:
+    """Give every process (in rank order) its wanted L3 domain index unless a
+    lower rank already holds it; then the first free domain on the same
+    socket (memory stays NUMA-local), else any free one, else share."""
+    taken: set = set()
+    out = []
+    for w in wanted:
+        choice = w
+        if w in taken:
+            pkg = package_of(min(doms[w])) if 0 <= w < len(doms) else 0
+            free = [i for i in range(len(doms)) if i not in taken]
+            same = [i for i in free if package_of(min(doms[i])) == pkg]
+            choice = (same or free or [w])[0]
+        taken.add(choice)
+        out.append(choice)
+    return out
