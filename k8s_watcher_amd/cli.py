@@ -9,7 +9,9 @@ Same contract as the reference:
 * an exception prints ``Error starting watcher: <e>``, exit 1.
 
 Fixes: Kubernetes setup failure exits 1 (reference: 0); SIGTERM stops the
-watcher gracefully like SIGINT; the watch ending on its own exits 0.
+watcher gracefully like SIGINT; the watch ending on its own exits 0. With
+``watcher.leader_election.enabled`` the process is one replica of several and
+watches only while it holds the Lease (``engine/leader.py``).
 Extra flags (all optional, after the environment): ``--config-dir``,
 ``--set key.path=value`` (repeatable), ``--print-config``, ``--check``
 (setup + connectivity only), ``--version``.
@@ -43,8 +45,11 @@ def _parser() -> argparse.ArgumentParser:
 
 
 async def _run_service(settings, check_only: bool) -> int:
+    from .engine.leader import LeaderElectedService, LeadershipLost
     from .engine.service import SetupError, WatcherService
     svc = WatcherService(settings)
+    if settings.watcher.leader_election.enabled and not check_only:
+        svc = LeaderElectedService(settings)
     if check_only:
         ok = await svc.setup_k8s_client()
         if svc.api is not None:
@@ -58,7 +63,7 @@ async def _run_service(settings, check_only: bool) -> int:
             pass
     try:
         await svc.run()
-    except SetupError:
+    except (SetupError, LeadershipLost):
         return 1
     return 0
 

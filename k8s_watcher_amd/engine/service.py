@@ -51,8 +51,9 @@ class SetupError(Exception):
 
 class WatcherService:
     def __init__(self, settings: Settings, endpoint: Optional[KubeEndpoint] = None,
-                 metrics: Optional[Metrics] = None, notifier_factory=None) -> None:
+                 metrics: Optional[Metrics] = None, notifier_factory=None, serve_metrics: bool = True) -> None:
         self.settings = settings
+        self.serve_metrics = serve_metrics  # False when an outer runner owns the metrics server
         self.endpoint = endpoint
         self.metrics = metrics or Metrics()
         self.notifier_factory = notifier_factory
@@ -187,7 +188,7 @@ class WatcherService:
                                              resource_version=rv, primed=bool(saved_rvs)))
         for r in self.reflectors:
             self._tasks.append(asyncio.ensure_future(r.run()))
-        if s.metrics.enabled:
+        if s.metrics.enabled and self.serve_metrics:
             self._metrics_server = await start_metrics_server(self.metrics, s.metrics.host, s.metrics.port)
         if ck:
             self._tasks.append(asyncio.ensure_future(self._checkpoint_loop()))
@@ -254,13 +255,23 @@ class WatcherService:
         for r in self.reflectors:
             r.stop()
 
-    async def shutdown(self, drain_timeout: float = 10.0) -> None:
+    async def shutdown(self, drain_timeout: float = 10.0, checkpoint: bool = True) -> None:
+        """Stop watching, drain the notifier, write the final checkpoint.
+
+        The checkpoint is written only if every notification was delivered:
+        a resourceVersion saved with notifications still queued would skip
+        them on restart; the previous (quiescent) checkpoint replays them
+        instead. ``checkpoint=False`` (a leader that lost its lease) never
+        writes — the new leader owns the file now.
+        """
         self.log.info("Stopping Pod watcher...")
         for r in self.reflectors:
             r.stop()
+        drained = True
         if self.notifier is not None:
-            await self.notifier.drain(drain_timeout)
-        await self._write_checkpoint()
+            drained = await self.notifier.drain(drain_timeout)
+        if checkpoint and drained:
+            await self._write_checkpoint()
         for t in self._tasks:
             if not t.done():
                 t.cancel()

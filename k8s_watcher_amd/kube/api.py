@@ -114,8 +114,42 @@ class KubeApi:
             raise ApiError(stream.status, stream.reason, err)
         return stream
 
+    # ------------------------------------------------------------------ coordination.k8s.io/v1
+    # Lease objects back leader election (engine/leader.py); the reference runs
+    # a single replica and has no equivalent.
+    async def _json(self, method: str, path: str, doc: Optional[Dict] = None,
+                    timeout: Optional[float] = None) -> Dict:
+        body = None if doc is None else json.dumps(doc, separators=(",", ":")).encode()
+        hdrs = None if body is None else {"Content-Type": "application/json"}
+        resp = await self.http.request(method, path, headers=hdrs, body=body, timeout=timeout)
+        if not resp.ok:
+            raise ApiError(resp.status, resp.reason, resp.body)
+        return resp.json() if resp.body else {}
+
+    async def get_lease(self, namespace: str, name: str, timeout: Optional[float] = None) -> Optional[Dict]:
+        """The Lease, or ``None`` when it does not exist."""
+        try:
+            return await self._json("GET", lease_path(namespace, name), timeout=timeout)
+        except ApiError as exc:
+            if exc.status == 404:
+                return None
+            raise
+
+    async def create_lease(self, namespace: str, lease: Dict, timeout: Optional[float] = None) -> Dict:
+        return await self._json("POST", lease_path(namespace), lease, timeout)
+
+    async def replace_lease(self, namespace: str, name: str, lease: Dict,
+                            timeout: Optional[float] = None) -> Dict:
+        """PUT; ``metadata.resourceVersion`` in ``lease`` makes it a compare-and-swap (409 on conflict)."""
+        return await self._json("PUT", lease_path(namespace, name), lease, timeout)
+
     async def close(self) -> None:
         await self.http.close()
+
+
+def lease_path(namespace: str, name: Optional[str] = None) -> str:
+    base = f"/apis/coordination.k8s.io/v1/namespaces/{namespace}/leases"
+    return f"{base}/{name}" if name else base
 
 
 def split_list_body(body: bytes) -> Tuple[Dict, list]:
@@ -124,4 +158,4 @@ def split_list_body(body: bytes) -> Tuple[Dict, list]:
     return doc.get("metadata") or {}, doc.get("items") or []
 
 
-__all__ = ["ApiError", "HttpError", "KubeApi", "pods_path", "split_list_body"]
+__all__ = ["ApiError", "HttpError", "KubeApi", "lease_path", "pods_path", "split_list_body"]

@@ -38,6 +38,10 @@ COUNTERS = (
     "relists",
     "expired_410",
     "checkpoints_written",
+    "leader_acquired",      # leadership terms started (engine/leader.py)
+    "leader_lost",
+    "lease_update_conflicts",
+    "lease_update_errors",
 )
 
 # 1 µs .. ~100 s, 4 buckets per decade (upper bounds in ns)

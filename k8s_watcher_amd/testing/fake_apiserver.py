@@ -14,6 +14,8 @@ be faithful where the watcher's correctness depends on it:
   the retained history after it; a compacted version → ``ERROR`` 410 event (or
   HTTP 410 with ``expired_as_http_status``); ``timeoutSeconds``;
   ``allowWatchBookmarks`` bookmarks on demand or periodically;
+* ``coordination.k8s.io/v1`` Leases (GET/POST/PUT/DELETE, compare-and-swap on
+  ``resourceVersion``) for leader election;
 * one HTTP chunk per event, as the real server flushes;
 * fault injection: drop every connection, expire every watch, fail the next
   N requests with a status, compact history, bearer-token auth (401).
@@ -39,6 +41,11 @@ from urllib.parse import parse_qs, urlsplit
 from ..utils.aio import with_timeout
 
 JSON = "application/json"
+
+
+LEASES_PREFIX = "/apis/coordination.k8s.io/v1/namespaces/"
+_REASONS = {200: "OK", 201: "Created", 400: "Bad Request", 404: "Not Found", 405: "Method Not Allowed",
+            409: "Conflict", 500: "Internal Server Error", 503: "Service Unavailable"}
 
 
 def _chunk(data: bytes) -> bytes:
@@ -141,6 +148,9 @@ class FakeApiServer:
         self.port = 0
         self.loop: Optional[asyncio.AbstractEventLoop] = None
         self._bm_task: Optional[asyncio.Task] = None
+        self.leases: Dict[Tuple[str, str], Dict[str, Any]] = {}
+        self.lease_writes: List[Tuple[Tuple[str, str], Dict[str, Any]]] = []
+        self.lease_fault: Optional[int] = None  # answer every lease request with this status
 
     # ------------------------------------------------------------------ lifecycle
     async def start(self, host: str = "127.0.0.1", port: int = 0, ssl_context=None) -> int:
@@ -305,14 +315,13 @@ class FakeApiServer:
                     k, _, v = h.decode("latin-1").partition(":")
                     headers[k.strip().lower()] = v.strip()
                 n = int(headers.get("content-length", "0") or 0)
-                if n:
-                    await reader.readexactly(n)
+                body = await reader.readexactly(n) if n else b""
                 parts = line.decode("latin-1").split()
                 if len(parts) < 2:
                     return
                 method, target = parts[0], parts[1]
                 self.requests.append((method, target))
-                keep = await self._route(method, target, headers, writer)
+                keep = await self._route(method, target, headers, writer, body)
                 if not keep:
                     return
         except (ConnectionError, asyncio.IncompleteReadError):
@@ -329,7 +338,8 @@ class FakeApiServer:
         writer.write(b"HTTP/1.1 %d %s\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n"
                      % (code, reason.encode(), len(body)) + body)
 
-    async def _route(self, method: str, target: str, headers: Dict[str, str], writer) -> bool:
+    async def _route(self, method: str, target: str, headers: Dict[str, str], writer,
+                     body: bytes = b"") -> bool:
         u = urlsplit(target)
         q = {k: v[-1] for k, v in parse_qs(u.query, keep_blank_values=True).items()}
         path = u.path
@@ -342,6 +352,10 @@ class FakeApiServer:
                 self.fail_next.pop(0)
                 self._send_json(writer, st, _status(st, "InternalError", "injected failure"), "Injected")
                 return True
+        if path.startswith(LEASES_PREFIX):
+            code, doc = self._lease(method, path[len(LEASES_PREFIX):], body)
+            self._send_json(writer, code, doc, _REASONS.get(code, "OK"))
+            return True
         if method != "GET":
             self._send_json(writer, 405, _status(405, "MethodNotAllowed", method), "Method Not Allowed")
             return True
@@ -370,6 +384,57 @@ class FakeApiServer:
                 and _match_fields(p, q.get("fieldSelector"))]
         self._send_json(writer, 200, self._paginate("PodList", pods, q))
         return True
+
+    # ------------------------------------------------------------------ leases
+    def _lease(self, method: str, rest: str, body: bytes) -> Tuple[int, Dict[str, Any]]:
+        """coordination.k8s.io/v1 Leases: GET/PUT/DELETE one, POST to the
+        collection; PUT with a stale ``metadata.resourceVersion`` → 409."""
+        ns, _, tail = rest.partition("/")
+        if not tail.startswith("leases"):
+            return 404, _status(404, "NotFound", rest)
+        name = tail[len("leases/"):] if tail.startswith("leases/") else ""
+        try:
+            doc = json.loads(body) if body else {}
+        except ValueError:
+            return 400, _status(400, "BadRequest", "invalid JSON body")
+        if self.lease_fault is not None:
+            code = self.lease_fault
+            return code, _status(code, "InternalError", "injected lease failure")
+        key = (ns, name or (doc.get("metadata") or {}).get("name", ""))
+        cur = self.leases.get(key)
+        if method == "GET" and name:
+            if cur is None:
+                return 404, _status(404, "NotFound", f'leases.coordination.k8s.io "{name}" not found')
+            return 200, copy.deepcopy(cur)
+        if method == "POST" and not name:
+            if cur is not None:
+                return 409, _status(409, "AlreadyExists", f'leases.coordination.k8s.io "{key[1]}" already exists')
+            return 201, self._store_lease(key, doc)
+        if method == "PUT" and name:
+            if cur is None:
+                return 404, _status(404, "NotFound", f'leases.coordination.k8s.io "{name}" not found')
+            want = (doc.get("metadata") or {}).get("resourceVersion")
+            if want and want != cur["metadata"]["resourceVersion"]:
+                return 409, _status(409, "Conflict", "the object has been modified; please apply your "
+                                                     "changes to the latest version and try again")
+            return 200, self._store_lease(key, doc)
+        if method == "DELETE" and name:
+            if self.leases.pop(key, None) is None:
+                return 404, _status(404, "NotFound", f'leases.coordination.k8s.io "{name}" not found')
+            return 200, _status(200, "", "deleted") | {"status": "Success"}
+        return 405, _status(405, "MethodNotAllowed", method)
+
+    def _store_lease(self, key: Tuple[str, str], doc: Dict[str, Any]) -> Dict[str, Any]:
+        obj = {"apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
+               "metadata": dict(doc.get("metadata") or {}), "spec": dict(doc.get("spec") or {})}
+        md = obj["metadata"]
+        md["namespace"], md["name"] = key
+        old = self.leases.get(key)
+        md["uid"] = old["metadata"]["uid"] if old else str(uuid.uuid4())
+        md["resourceVersion"] = str(self._next_rv())
+        self.leases[key] = obj
+        self.lease_writes.append((key, copy.deepcopy(obj["spec"])))
+        return copy.deepcopy(obj)
 
     def _paginate(self, kind: str, items: List[Dict[str, Any]], q: Dict[str, str]) -> Dict[str, Any]:
         start = 0

@@ -241,6 +241,21 @@ class MetricsSettings:
 
 
 @dataclass
+class LeaderElectionSettings:
+    """``watcher.leader_election`` (engine/leader.py): one active replica of several."""
+
+    enabled: bool = False
+    lease_name: str = "k8s-watcher-amd"
+    lease_namespace: Optional[str] = None  # None = the pod's namespace, else "default"
+    identity: Optional[str] = None  # None = $POD_NAME, else <hostname>_<random>
+    lease_duration_seconds: float = 15.0
+    renew_deadline_seconds: float = 10.0
+    retry_period_seconds: float = 2.0
+    release_on_shutdown: bool = True
+    exit_on_loss: bool = False
+
+
+@dataclass
 class WatcherSettings:
     log_level: str = "INFO"
     log_file: Optional[str] = None
@@ -264,6 +279,7 @@ class WatcherSettings:
     log_events: Optional[bool] = None  # None = follow log level (parity)
     checkpoint: CheckpointSettings = field(default_factory=CheckpointSettings)
     shard: "ShardSettings" = field(default_factory=lambda: ShardSettings())
+    leader_election: LeaderElectionSettings = field(default_factory=LeaderElectionSettings)
 
 
 @dataclass
@@ -312,6 +328,26 @@ def _shard(block: Dict[str, Any]) -> ShardSettings:
     if s.count < 1 or not 0 <= s.index < s.count:
         raise ConfigError(f"watcher.shard: index {s.index} outside [0, {s.count})")
     return s
+
+
+def _leader_election(block: Dict[str, Any]) -> LeaderElectionSettings:
+    key = "watcher.leader_election"
+    le = LeaderElectionSettings(
+        enabled=_as_bool(block.get("enabled", False), f"{key}.enabled"),
+        lease_name=str(block.get("lease_name") or "k8s-watcher-amd"),
+        lease_namespace=block.get("lease_namespace") or None,
+        identity=block.get("identity") or None,
+        lease_duration_seconds=_as_float(block.get("lease_duration_seconds", 15), f"{key}.lease_duration_seconds"),
+        renew_deadline_seconds=_as_float(block.get("renew_deadline_seconds", 10), f"{key}.renew_deadline_seconds"),
+        retry_period_seconds=_as_float(block.get("retry_period_seconds", 2), f"{key}.retry_period_seconds"),
+        release_on_shutdown=_as_bool(block.get("release_on_shutdown", True), f"{key}.release_on_shutdown"),
+        exit_on_loss=_as_bool(block.get("exit_on_loss", False), f"{key}.exit_on_loss"),
+    )
+    if not 0 < le.retry_period_seconds < le.renew_deadline_seconds < le.lease_duration_seconds:
+        raise ConfigError(f"{key}: need 0 < retry_period_seconds < renew_deadline_seconds < "
+                          f"lease_duration_seconds, got {le.retry_period_seconds} / "
+                          f"{le.renew_deadline_seconds} / {le.lease_duration_seconds}")
+    return le
 
 
 def _decode_threads(v: Any) -> int:
@@ -372,6 +408,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
             interval_seconds=_as_float(ck.get("interval_seconds", 5.0), "watcher.checkpoint.interval_seconds"),
         ),
         shard=_shard(w.get("shard") or {}),
+        leader_election=_leader_election(w.get("leader_election") or {}),
     )
 
     endpoints = c.get("endpoints") or {}

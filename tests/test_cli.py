@@ -149,3 +149,53 @@ def test_podwatcher_filters_like_reference(tmp_path):
     assert w.handle_pod_event("DELETED", running)["event_type"] == "DELETED"
     assert w.handle_pod_event("MODIFIED", failed)["status"]["phase"] == "Failed"
     assert w.handle_pod_event("MODIFIED", other_ns) is None
+
+
+def test_two_replicas_leader_election_cli(cluster):
+    """Two ``main.py`` processes with leader election: one watches; SIGTERM on it
+    releases the lease and the other takes over (lists and logs the pods)."""
+    st, srv, cfg = cluster
+    e = dict(os.environ)
+    e.pop("ENVIRONMENT", None)
+    sets = ["--set", "watcher.leader_election.enabled=true", "--set", "watcher.leader_election.lease_namespace=default",
+            "--set", "watcher.leader_election.lease_duration_seconds=4",
+            "--set", "watcher.leader_election.renew_deadline_seconds=3",
+            "--set", "watcher.leader_election.retry_period_seconds=0.2"]
+
+    def start(name):
+        return subprocess.Popen([sys.executable, MAIN, "staging", "--config-dir", cfg, *sets,
+                                 "--set", f"watcher.leader_election.identity={name}"],
+                                stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=e, cwd=ROOT)
+
+    def watches():
+        return sum(1 for _, t in srv.requests if "/api/v1/pods" in t and "watch=true" in t)
+
+    def wait_for(pred, limit=30):
+        deadline = time.time() + limit
+        while time.time() < deadline and not pred():
+            time.sleep(0.05)
+        assert pred()
+
+    a = start("replica-a")
+    b = None
+    try:
+        wait_for(lambda: watches() == 1)
+        b = start("replica-b")
+        wait_for(lambda: any(t.endswith("/leases/k8s-watcher-amd") and m == "GET" for m, t in srv.requests[-5:]))
+        time.sleep(1.0)
+        assert watches() == 1  # b is a standby
+        a.send_signal(signal.SIGTERM)
+        out_a, err_a = a.communicate(timeout=20)
+        assert a.returncode == 0, err_a
+        assert "Released lease default/k8s-watcher-amd" in err_a
+        wait_for(lambda: watches() == 2)
+        time.sleep(0.5)
+        b.send_signal(signal.SIGTERM)
+        out_b, err_b = b.communicate(timeout=20)
+    finally:
+        for p in (a, b):
+            if p is not None and p.poll() is None:
+                p.kill()
+    assert b.returncode == 0, err_b
+    assert "Acquired leadership of lease default/k8s-watcher-amd as replica-b" in err_b
+    assert err_b.count("Pod event detected: ADDED - default/") == 3
