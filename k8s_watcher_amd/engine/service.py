@@ -37,6 +37,7 @@ from ..ops.decode import make_decoder
 from ..parallel.native_notifier import NativeNotifierPool
 from ..parallel.notifier import NotifierPool, NullNotifier
 from ..parallel.shard import ShardFilter
+from ..parallel.spool import Spool, SpoolReplayer
 from ..utils.config import Settings
 from ..utils.fastlog import EventLog
 from ..utils.logsetup import SERVICE_LOGGER
@@ -69,6 +70,8 @@ class WatcherService:
         self._metrics_server = None
         self.started = asyncio.Event()
         self.server_version: Optional[str] = None
+        self.spool = None
+        self.spool_replayer = None
 
     # ------------------------------------------------------------------ setup
     def load_endpoint(self) -> KubeEndpoint:
@@ -152,6 +155,17 @@ class WatcherService:
                 self.log.warning("ClusterAPI health check failed, but continuing...")
         if s.clusterapi.enabled and hasattr(self.notifier, "warm_up"):
             await self.notifier.warm_up()
+        sp = s.clusterapi.spool
+        if s.clusterapi.enabled and sp.path and hasattr(self.notifier, "attach_spool"):
+            self.spool = Spool(sp.path, sp.max_bytes, sp.segment_bytes, sp.fsync, self.metrics)
+            self.notifier.attach_spool(self.spool)
+            self.metrics.gauges["spool_records"] = lambda: float(len(self.spool))
+            self.metrics.gauges["spool_bytes"] = lambda: float(self.spool.bytes)
+            if len(self.spool):
+                self.log.warning(f"Spool {sp.path} holds {len(self.spool)} notifications from an earlier run")
+            self.spool_replayer = SpoolReplayer(self.spool, self.notifier, self.metrics,
+                                                sp.replay_interval_seconds, sp.replay_batch)
+            self._tasks.append(asyncio.ensure_future(self.spool_replayer.run()))
         self.decoder = make_decoder(s.watcher.engine, s.environment, s.watcher.state_format)
         scopes = (ShardFilter(s.watcher.shard).namespaces(s.watcher.namespaces)
                   if s.watcher.namespace_scope == "server" and s.watcher.namespaces else [None])
@@ -283,7 +297,9 @@ class WatcherService:
         if self._metrics_server is not None:
             self._metrics_server.close()
         if self.notifier is not None:
-            await self.notifier.close()
+            await self.notifier.close()  # with a spool, whatever is still owed is written to it
+        if self.spool is not None:
+            self.spool.close()
         if self.api is not None:
             await self.api.close()
 

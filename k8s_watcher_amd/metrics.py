@@ -34,6 +34,10 @@ COUNTERS = (
     "notify_retried",
     "notify_superseded",
     "notify_coalesced",
+    "notify_spooled",       # owed notifications written to the spool (parallel/spool.py)
+    "spool_replayed",
+    "spool_stale_skipped",
+    "spool_dropped",
     "watch_restarts",
     "relists",
     "expired_410",

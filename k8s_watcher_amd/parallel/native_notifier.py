@@ -24,6 +24,7 @@ import array
 import asyncio
 import logging
 import socket
+import time
 from typing import Callable, Dict, Optional
 from urllib.parse import urlsplit
 
@@ -80,7 +81,34 @@ class NativeNotifierPool:
         self.saturated = False
         self.on_saturation = on_saturation
         self.closing = False
+        self.spool = None
         self._watchdog = self.loop.create_task(self._watchdog_loop())
+
+    # ------------------------------------------------------------------ spool (parallel/spool.py)
+    def attach_spool(self, spool) -> None:
+        """Owed notifications go to ``spool`` instead of being dropped."""
+        self.spool = spool
+        self.core.spool_control(True)
+        for uid in spool.uid_counts:
+            self.core.spool_watch(uid, True)
+
+    def replay(self, records) -> int:
+        """Resubmit spooled records that are not stale; returns how many were submitted."""
+        n = 0
+        now = time.monotonic_ns()
+        core = self.core
+        for r in records:
+            if core.spool_stale(r.uid, r.seq):
+                continue
+            core.submit_body(r.uid, r.etype, r.ns, r.name, r.body, now)
+            n += 1
+        return n
+
+    def replay_pending(self) -> int:
+        return self.core.replay_pending()
+
+    def spool_unwatch(self, uid: str) -> None:
+        self.core.spool_watch(uid, False)
 
     # ------------------------------------------------------------------ API (NotifierPool-compatible)
     def submit(self, uid, etype, ns, name, core: bytes, read_ns: int, ts: str) -> None:
@@ -205,7 +233,10 @@ class NativeNotifierPool:
         self._after()
 
     def _after(self, connect_failed: Optional[int] = None) -> None:
-        retries, logs, need_connect, want_write, lost, lat = self.core.take()
+        retries, logs, need_connect, want_write, lost, lat, spooled = self.core.take()
+        if spooled:
+            for uid in self.spool.append(spooled):
+                self.core.spool_watch(uid, True)
         for i in lost:
             self._drop_socket(i)
         for seq, delay in retries:

@@ -253,7 +253,49 @@ class NotifierPool:
         self._dirty: List[_Conn] = []
         self._flush_scheduled = False
         self.retry_policy = settings.retry
+        # spool (parallel/spool.py): uid -> seq of the newest live submit, for uids with spooled records
+        self.spool = None
+        self.spool_watch: Dict[str, int] = {}
+        self.replaying: Dict[int, NotifyRequest] = {}
+        self.retrying: Dict[int, NotifyRequest] = {}
         self._watchdog = self.loop.create_task(self._watchdog_loop())
+
+    # ------------------------------------------------------------------ spool
+    def attach_spool(self, spool) -> None:
+        """Owed notifications go to ``spool`` instead of being dropped."""
+        self.spool = spool
+        for uid in spool.uid_counts:
+            self.spool_watch.setdefault(uid, 0)
+
+    def replay(self, records) -> int:
+        """Resubmit spooled records that are not stale; returns how many were submitted."""
+        n = 0
+        now = time.monotonic_ns()
+        for r in records:
+            if self.spool_watch.get(r.uid, 0) > r.seq:
+                continue
+            self.seq += 1
+            conn = self.conns[zlib.crc32(r.uid.encode()) % len(self.conns)] if r.uid else self.conns[0]
+            req = NotifyRequest(r.uid, self.seq, r.etype, r.ns, r.name, r.body, now, conn)
+            self.latest[r.uid] = req.seq
+            self.replaying[req.seq] = req
+            conn.queue.append(req)
+            self._dirty.append(conn)
+            self.metrics.c["notify_submitted"] += 1
+            self._add_pending(1)
+            n += 1
+        return n
+
+    def replay_pending(self) -> int:
+        return len(self.replaying)
+
+    def spool_unwatch(self, uid: str) -> None:
+        self.spool_watch.pop(uid, None)
+
+    def _finish(self, req: NotifyRequest) -> None:
+        if self.replaying:
+            self.replaying.pop(req.seq, None)
+        self._add_pending(-1)
 
     # ------------------------------------------------------------------ public API
     def submit(self, uid: str, etype: str, ns: Optional[str], name: Optional[str], core: bytes,
@@ -262,6 +304,8 @@ class NotifierPool:
         body = finish_body(core, etype, ts)
         m = self.metrics.c
         m["notify_submitted"] += 1
+        if self.spool_watch and uid in self.spool_watch:
+            self.spool_watch[uid] = self.seq + 1  # the seq this submit gets (or coalesces into)
         if self.settings.pool.coalesce:
             old = self.unsent.get(uid)
             if old is not None:
@@ -340,11 +384,19 @@ class NotifierPool:
     async def close(self) -> None:
         self.closing = True
         self._watchdog.cancel()
+        owed: List[NotifyRequest] = list(self.retrying.values())
+        self.retrying.clear()
         for c in self.conns:
             if c.reconnect_handle is not None:
                 c.reconnect_handle.cancel()
+            owed.extend(c.inflight)
+            owed.extend(c.queue)
+            c.inflight.clear()
+            c.queue.clear()
             if c.transport is not None:
                 c.transport.close()
+        for req in owed:  # still outstanding: fail (or spool) them, as the native core does
+            self._give_up(req, spoolable=True)
         await asyncio.sleep(0)
 
     def outstanding(self) -> int:
@@ -375,7 +427,7 @@ class NotifierPool:
         if self.log_events:
             self.elog.log(logging.INFO,
                           f"Successfully notified clusterapi about {req.etype} event for {req.ns}/{req.name}")
-        self._add_pending(-1)
+        self._finish(req)
 
     def _failed(self, req: NotifyRequest, status: Optional[int], detail: str) -> None:
         if status is not None:
@@ -385,29 +437,38 @@ class NotifierPool:
         retryable = status is None or status in RETRYABLE_STATUS
         if self.latest.get(req.uid) != req.seq:
             self.metrics.c["notify_superseded"] += 1
-            self._add_pending(-1)
+            self._finish(req)
             return
         if retryable and req.attempts < self.retry_policy.max_attempts and not self.closing:
             self.metrics.c["notify_retried"] += 1
             delay = self.retry_policy.delay(req.attempts)
+            self.retrying[req.seq] = req
             self.loop.call_later(delay, self._retry_fire, req)
             return
-        self._give_up(req)
+        self._give_up(req, spoolable=retryable)
 
-    def _give_up(self, req: NotifyRequest) -> None:
-        self.metrics.c["notify_failed"] += 1
+    def _give_up(self, req: NotifyRequest, spoolable: bool = False) -> None:
         if self.latest.get(req.uid) == req.seq:
             del self.latest[req.uid]
-        self.svc_log.error(f"Failed to notify clusterapi about {req.etype} event for {req.ns}/{req.name}")
-        self._add_pending(-1)
+        if self.spool is not None and spoolable:
+            self.metrics.c["notify_spooled"] += 1
+            for uid in self.spool.append([(req.uid, req.etype, req.ns if req.ns is not None else "None",
+                                           req.name if req.name is not None else "None", req.body, req.seq)]):
+                self.spool_watch.setdefault(uid, 0)
+        else:
+            self.metrics.c["notify_failed"] += 1
+            self.svc_log.error(f"Failed to notify clusterapi about {req.etype} event for {req.ns}/{req.name}")
+        self._finish(req)
 
     def _retry_fire(self, req: NotifyRequest) -> None:
+        if self.retrying.pop(req.seq, None) is None:
+            return  # already given up (pool closed)
         if self.latest.get(req.uid) != req.seq:
             self.metrics.c["notify_superseded"] += 1
-            self._add_pending(-1)
+            self._finish(req)
             return
         if self.closing:
-            self._give_up(req)
+            self._give_up(req, spoolable=True)
             return
         conn = req.conn
         conn.queue.appendleft(req)

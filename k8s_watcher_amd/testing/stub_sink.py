@@ -8,7 +8,7 @@ The reference ships no clusterapi stub. This one:
 * records bodies (``record=True``) with their receive time so tests can
   check schema, per-pod order and exactly-once delivery;
 * injects latency (fixed seconds) and failures (a status for a fraction of
-  requests, or for the next N requests);
+  requests, or for the next N requests, or an outage with ``state.down``);
 * is a raw ``asyncio.Protocol`` so that, in benchmarks, it is not the
   bottleneck; :func:`run_sink_process` runs several SO_REUSEPORT workers.
 """
@@ -58,6 +58,7 @@ class SinkState:
         self.health_checks = 0
         self.connections = 0
         self.waiters: List[Tuple[int, asyncio.Future]] = []
+        self.down = False  # outage: /health and every POST answer 503
 
     def payloads(self) -> List[Dict]:
         return [json.loads(b) for _, b in self.received]
@@ -121,13 +122,16 @@ class _SinkProtocol(asyncio.Protocol):
             method, path = head[:sp1], head[sp1 + 1:sp2]
             if method == b"GET" and path.startswith(b"/health"):
                 st.health_checks += 1
-                responses.append(_resp(200, b'{"status":"healthy"}'))
+                responses.append(_resp(503, b'{"status":"down"}') if st.down
+                                 else _resp(200, b'{"status":"healthy"}'))
                 continue
             if method != b"POST" or path != st.path:
                 responses.append(_resp(404, b'{"error":"not found"}'))
                 continue
             fail = None
-            if st.fail_next:
+            if st.down:
+                fail = 503
+            elif st.fail_next:
                 fail = st.fail_next.pop(0)
             elif st.fail_rate and st.rng.random() < st.fail_rate:
                 fail = st.fail_status

@@ -213,6 +213,18 @@ class NotifierPoolSettings:
 
 
 @dataclass
+class SpoolSettings:
+    """``clusterapi.spool`` (parallel/spool.py): durable log of owed notifications."""
+
+    path: Optional[str] = None  # None = off (reference: failed notifications are dropped)
+    max_bytes: int = 1 << 30
+    segment_bytes: int = 64 << 20
+    fsync: bool = False
+    replay_interval_seconds: float = 5.0
+    replay_batch: int = 1000
+
+
+@dataclass
 class ClusterApiSettings:
     enabled: bool = True
     base_url: str = "http://localhost:3000"
@@ -225,6 +237,7 @@ class ClusterApiSettings:
     verify_tls: bool = True
     ca_file: Optional[str] = None
     health_check_on_start: bool = True
+    spool: SpoolSettings = field(default_factory=SpoolSettings)
 
 
 @dataclass
@@ -330,6 +343,21 @@ def _shard(block: Dict[str, Any]) -> ShardSettings:
     return s
 
 
+def _spool(block: Dict[str, Any]) -> SpoolSettings:
+    key = "clusterapi.spool"
+    sp = SpoolSettings(
+        path=block.get("path") or None,
+        max_bytes=_as_int(block.get("max_bytes", 1 << 30), f"{key}.max_bytes"),
+        segment_bytes=_as_int(block.get("segment_bytes", 64 << 20), f"{key}.segment_bytes"),
+        fsync=_as_bool(block.get("fsync", False), f"{key}.fsync"),
+        replay_interval_seconds=_as_float(block.get("replay_interval_seconds", 5), f"{key}.replay_interval_seconds"),
+        replay_batch=_as_int(block.get("replay_batch", 1000), f"{key}.replay_batch"),
+    )
+    if sp.max_bytes <= 0 or sp.segment_bytes <= 0 or sp.replay_batch <= 0 or sp.replay_interval_seconds <= 0:
+        raise ConfigError(f"{key}: sizes, batch and interval must be positive")
+    return sp
+
+
 def _leader_election(block: Dict[str, Any]) -> LeaderElectionSettings:
     key = "watcher.leader_election"
     le = LeaderElectionSettings(
@@ -432,6 +460,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         verify_tls=_as_bool(c.get("verify_tls", True), "clusterapi.verify_tls"),
         ca_file=c.get("ca_file") or None,
         health_check_on_start=_as_bool(c.get("health_check_on_start", True), "clusterapi.health_check_on_start"),
+        spool=_spool(c.get("spool") or {}),
     )
 
     metrics = MetricsSettings(

@@ -7,6 +7,7 @@ import random
 
 import pytest
 
+from conftest import ROOT
 from k8s_watcher_amd.engine.pipeline import EventPipeline
 from k8s_watcher_amd.metrics import Metrics
 from k8s_watcher_amd.ops.decode import PyDecoder
@@ -180,3 +181,20 @@ def test_decode_pool_lifecycle():
     assert os_threads() == before
     with pytest.raises(ValueError):
         mod.Pipeline("production", mod.PodCache(), {}, None, True, False, 1, 0, True, True, None, False, False, 65)
+
+
+def test_decode_pool_create_destroy_race():
+    """Workers the OS schedules only after the pool was used or destroyed must
+    still see that wake-up (a late-starting worker used to sleep forever and
+    hang the destructor's join). Run in a child so a regression fails, not hangs."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from k8s_watcher_amd.ops.native import load\n"
+            "m = load()\n"
+            "for i in range(300):\n"
+            "    p = m.DecodePool(1 + i %% 8)\n"
+            "    del p\n"
+            "print('ok')\n") % ROOT
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stderr

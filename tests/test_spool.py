@@ -1,0 +1,211 @@
+"""Durable notification spool (parallel/spool.py), on both notifier pools.
+
+The reference drops a notification whose POST fails
+(``/root/reference/watcher/clusterapi_client.py:38-53``). With
+``clusterapi.spool.path`` owed notifications survive a clusterapi outage and
+a restart, are replayed in order, and never overwrite newer state.
+"""
+
+import asyncio
+import json
+import os
+
+import pytest
+
+from conftest import run
+from k8s_watcher_amd.metrics import Metrics
+from k8s_watcher_amd.parallel.native_notifier import NativeNotifierPool
+from k8s_watcher_amd.parallel.notifier import NotifierPool
+from k8s_watcher_amd.parallel.spool import Spool, SpoolReplayer
+from k8s_watcher_amd.testing.stub_sink import StubSink
+from test_notifier import TS, core, settings
+
+
+def rec(uid, body=b"{}", seq=1, etype="MODIFIED"):
+    return (uid, etype, "default", f"p-{uid}", body, seq)
+
+
+# ---------------------------------------------------------------------- storage
+def test_append_read_commit_and_reopen(tmp_path):
+    sp = Spool(str(tmp_path), segment_bytes=200)
+    assert sp.append([rec(f"u{i}", b'{"i":%d}' % i, i + 1) for i in range(10)]) == [f"u{i}" for i in range(10)]
+    assert len(sp) == 10 and sp.tail > 0  # rotated over several segments
+    got, pos = sp.read_batch(4)
+    assert [r.uid for r in got] == ["u0", "u1", "u2", "u3"] and got[0].seq == 1
+    assert sp.commit(pos, got) == ["u0", "u1", "u2", "u3"]
+    sp.close()
+    sp2 = Spool(str(tmp_path), segment_bytes=200)
+    assert len(sp2) == 6 and set(sp2.uid_counts) == {f"u{i}" for i in range(4, 10)}
+    got, pos = sp2.read_batch(100)
+    assert [json.loads(r.body)["i"] for r in got] == list(range(4, 10))
+    assert all(r.seq == 0 for r in got)  # written by an earlier process: older than anything live
+    sp2.commit(pos, got)
+    assert len(sp2) == 0 and sp2.bytes == 0
+    assert len([f for f in os.listdir(tmp_path) if f.endswith(".spool")]) == 1
+    sp2.append([rec("again")])
+    got, _ = sp2.read_batch(10)
+    assert [r.uid for r in got] == ["again"]
+    sp2.close()
+
+
+def test_torn_tail_and_size_limit(tmp_path):
+    sp = Spool(str(tmp_path))
+    sp.append([rec("a"), rec("b")])
+    sp.close()
+    seg = sorted(f for f in os.listdir(tmp_path) if f.endswith(".spool"))[-1]
+    with open(tmp_path / seg, "ab") as fh:
+        fh.write(b"\x10\x00\x00\x00\x05")  # crash mid-append
+    sp = Spool(str(tmp_path), max_bytes=200)
+    assert len(sp) == 2
+    got, _ = sp.read_batch(10)
+    assert [r.uid for r in got] == ["a", "b"]
+    m = sp.metrics
+    sp.append([rec("big", b"x" * 500)])
+    assert m.c["spool_dropped"] == 1 and len(sp) == 2
+    sp.close()
+
+
+# ---------------------------------------------------------------------- pools
+@pytest.fixture(params=["python", "native"])
+def pool_cls(request):
+    return NotifierPool if request.param == "python" else NativeNotifierPool
+
+
+async def spool_stack(cls, path, **kw):
+    sink = StubSink()
+    await sink.start()
+    m = Metrics()
+    kw = {"attempts": 2, "delay": 0.01, **kw}
+    pool = cls(settings(sink.url, **kw), m)
+    sp = Spool(str(path), metrics=m)
+    pool.attach_spool(sp)
+    return sink, pool, m, sp
+
+
+def test_outage_spools_then_replays_in_order(pool_cls, tmp_path):
+    async def body():
+        sink, pool, m, sp = await spool_stack(pool_cls, tmp_path)
+        sink.state.down = True
+        for i in range(30):
+            pool.submit(f"u{i % 5}", "MODIFIED", "default", f"p{i % 5}", core(f"u{i % 5}", name=f"v{i}"), 0, TS)
+            pool.flush()
+            await asyncio.sleep(0)
+        assert await pool.drain(5)
+        # superseded ones are dropped; each pod's newest notification is owed
+        assert m.c["notify_failed"] == 0 and m.c["notify_spooled"] >= 5 and len(sp) == m.c["notify_spooled"]
+        rp = SpoolReplayer(sp, pool, m, interval=0.01)
+        assert not await pool.health_check()
+        sink.state.down = False
+        assert await pool.health_check()
+        assert await asyncio.wait_for(rp.replay_once(), 10)
+        assert len(sp) == 0
+        last = {}
+        for p in sink.state.payloads():
+            last[p["uid"]] = p["name"]
+        # the final state of every pod reached clusterapi
+        assert last == {f"u{k}": f"v{25 + k}" for k in range(5)}
+        await pool.close()
+        sp.close()
+        await sink.stop()
+    run(body())
+
+
+def test_replay_skips_records_overtaken_by_live_state(pool_cls, tmp_path):
+    async def body():
+        sink, pool, m, sp = await spool_stack(pool_cls, tmp_path)
+        sink.state.down = True
+        pool.submit("a", "MODIFIED", "default", "pa", core("a", name="old-a"), 0, TS)
+        pool.submit("b", "MODIFIED", "default", "pb", core("b", name="old-b"), 0, TS)
+        pool.flush()
+        assert await pool.drain(5)
+        assert len(sp) == 2
+        sink.state.down = False
+        # a newer live event for "a" is delivered before the spool is replayed
+        pool.submit("a", "MODIFIED", "default", "pa", core("a", name="new-a"), 0, TS)
+        pool.flush()
+        assert await pool.drain(5)
+        assert await SpoolReplayer(sp, pool, m).replay_once()
+        names = [p["name"] for p in sink.state.payloads()]
+        assert names == ["new-a", "old-b"]
+        assert m.c["spool_stale_skipped"] == 1 and m.c["spool_replayed"] == 1
+        await pool.close()
+        sp.close()
+        await sink.stop()
+    run(body())
+
+
+def test_close_spools_outstanding_and_restart_replays(pool_cls, tmp_path):
+    async def body():
+        sink, pool, m, sp = await spool_stack(pool_cls, tmp_path, attempts=50)
+        sink.state.down = True
+        for i in range(8):
+            pool.submit(f"u{i}", "ADDED", "default", f"p{i}", core(f"u{i}"), 0, TS)
+        pool.flush()
+        await asyncio.sleep(0.1)
+        assert pool.outstanding() == 8  # still retrying
+        await pool.close()  # shutdown with notifications owed
+        assert len(sp) == 8 and m.c["notify_failed"] == 0
+        sp.close()
+        sink.state.down = False
+        # "restart": a new pool and spool on the same directory
+        m2 = Metrics()
+        pool2 = pool_cls(settings(sink.url), m2)
+        sp2 = Spool(str(tmp_path), metrics=m2)
+        pool2.attach_spool(sp2)
+        assert len(sp2) == 8
+        assert await SpoolReplayer(sp2, pool2, m2).replay_once()
+        assert sorted(p["uid"] for p in sink.state.payloads()) == [f"u{i}" for i in range(8)]
+        assert len(sp2) == 0
+        await pool2.close()
+        sp2.close()
+        await sink.stop()
+    run(body())
+
+
+def test_non_retryable_failures_are_not_spooled(pool_cls, tmp_path):
+    async def body():
+        sink, pool, m, sp = await spool_stack(pool_cls, tmp_path)
+        sink.state.fail_next = [400]
+        pool.submit("x", "ADDED", "default", "px", core("x"), 0, TS)
+        pool.flush()
+        assert await pool.drain(5)
+        assert m.c["notify_failed"] == 1 and len(sp) == 0
+        await pool.close()
+        sp.close()
+        await sink.stop()
+    run(body())
+
+
+# ---------------------------------------------------------------------- service
+def test_service_outage_recovery_with_spool(tmp_path):
+    from test_e2e_slice import start_stack
+    from k8s_watcher_amd.testing.podgen import PodFactory
+
+    async def body():
+        ov = {"clusterapi": {"retry": {"max_attempts": 2}, "spool": {"path": str(tmp_path / "spool"),
+                                                                     "replay_interval_seconds": 0.05}}}
+        srv, sink, svc = await start_stack("staging", overrides=ov)
+        await svc.start()
+        f = PodFactory(seed=3, namespaces=["default"])
+        sink.state.down = True
+        pods = [f.running(f.new_pod()) for _ in range(6)]
+        for p in pods:
+            srv.create(p)
+        for _ in range(200):
+            if svc.metrics.c["notify_spooled"] >= 6:
+                break
+            await asyncio.sleep(0.02)
+        assert svc.metrics.c["notify_spooled"] == 6 and sink.state.count == 0
+        sink.state.down = False
+        await sink.state.wait_for(6, timeout=10)
+        for _ in range(100):
+            if len(svc.spool) == 0:
+                break
+            await asyncio.sleep(0.02)
+        assert len(svc.spool) == 0
+        assert sorted(p["uid"] for p in sink.state.payloads()) == sorted(p["metadata"]["uid"] for p in pods)
+        svc.stop()
+        await svc.shutdown()
+        await sink.stop()
+        await srv.stop()
+    run(body())
