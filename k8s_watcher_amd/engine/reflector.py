@@ -17,6 +17,9 @@ This reflector:
   resourceVersion with no relist;
 * on ``410 Gone`` (HTTP status or ``ERROR`` event) relists and reconciles, so
   no state change is lost and unchanged pods are not re-notified;
+* with ``watcher.initial_sync: watch_list`` gets the state as a WatchList
+  stream (``sendInitialEvents``) instead of a LIST, falling back to LIST on
+  API servers without it;
 * on transport errors backs off per ``watcher.retry`` and gives up after
   ``max_attempts`` consecutive failures (0 = never), raising
   :class:`WatchFailed`;
@@ -33,7 +36,7 @@ from typing import Optional
 from ..kube.api import ApiError, KubeApi
 from ..metrics import Metrics
 from ..net.http import HttpError
-from ..ops.decode import E_EXTRA, E_TYPE, ERROR, INVALID
+from ..ops.decode import ADDED, BOOKMARK, DELETED, E_EXTRA, E_RV, E_TYPE, E_UID, ERROR, INVALID, MODIFIED
 from ..utils.backoff import Backoff
 from ..utils.config import Settings
 from ..utils.logsetup import SERVICE_LOGGER
@@ -46,6 +49,10 @@ class Expired(Exception):
 
 class WatchFailed(Exception):
     """Consecutive watch failures exhausted ``watcher.retry.max_attempts``."""
+
+
+class WatchListUnsupported(Exception):
+    """The API server refused ``sendInitialEvents`` or never ended the initial events."""
 
 
 class Reflector:
@@ -67,6 +74,7 @@ class Reflector:
         self.connected = asyncio.Event()
         self.synced = asyncio.Event()
         self.watch_count = 0
+        self.watch_list = settings.watcher.initial_sync == "watch_list"
 
     @property
     def scope(self) -> str:
@@ -111,6 +119,107 @@ class Reflector:
             self._handle_control(ev)
         self.rv = list_rv
         self.pipeline.last_rv = list_rv
+        self.synced.set()
+
+    async def sync(self, notify: bool = True) -> None:
+        """Initial / post-410 state: WatchList when configured and supported, else LIST."""
+        if self.watch_list:
+            try:
+                await self.watch_list_sync(notify)
+                return
+            except WatchListUnsupported as exc:
+                self.watch_list = False  # do not ask again in this process
+                self.log.warning(f"WatchList unavailable ({exc}); falling back to LIST")
+        await self.relist(notify=notify)
+
+    async def watch_list_sync(self, notify: bool = True) -> None:
+        """Streamed initial state (``sendInitialEvents=true``, KEP-3157).
+
+        The API server serves the current state from its watch cache as
+        ``ADDED`` events and closes it with a bookmark annotated
+        ``k8s.io/initial-events-end`` — no large LIST response has to be built
+        server-side. The events are collected until that bookmark and then
+        reconciled against the pod cache exactly like a LIST (unchanged pods
+        are not re-notified, vanished ones become ``DELETED``); the stream is
+        closed there and the regular watch resumes from the bookmark's
+        resourceVersion.
+        """
+        w = self.settings.watcher
+        decoder = self.decoder
+        decoder.reset()
+        state: dict = {}
+        end: list = []
+        framed = [False]
+        errors: list = []
+
+        def on_mode(is_framed: bool) -> None:
+            framed[0] = is_framed
+
+        def sink(data: bytes, read_ns: int) -> None:
+            if end or errors:
+                return
+            evs = decoder.feed_chunked(data) if framed[0] else decoder.feed(data)
+            for ev in evs:
+                t = ev[E_TYPE]
+                if t == ADDED or t == MODIFIED:
+                    state[ev[E_UID]] = ev
+                elif t == DELETED:
+                    state.pop(ev[E_UID], None)
+                elif t == BOOKMARK:
+                    if ev[E_EXTRA] is True:
+                        end.append(ev[E_RV])
+                        break
+                elif t == ERROR:
+                    errors.append(ev[E_EXTRA] or {})
+                    break
+                else:
+                    self._handle_control(ev)
+            if (end or errors) and self.stream is not None:
+                self.stream.close()
+
+        try:
+            self.stream = await self.api.watch_pods(
+                sink, namespace=self.namespace, send_initial_events=True,
+                label_selector=w.label_selector, field_selector=w.field_selector,
+                raw_chunked=True, on_mode=on_mode)
+        except ApiError as exc:
+            if exc.status == 410:
+                raise
+            if 400 <= exc.status < 500:
+                raise WatchListUnsupported(str(exc)) from None
+            raise
+        try:
+            finished = self.stream.finished
+            idle = w.watch_list_idle_seconds
+            while not finished.done() and not end and not errors and not self._stop.is_set():
+                await asyncio.wait([finished], timeout=min(1.0, idle))
+                if (not finished.done() and not end
+                        and time.monotonic() - self.stream.last_activity > idle):
+                    # an API server that ignores sendInitialEvents streams the
+                    # state and then goes quiet without the end marker
+                    raise WatchListUnsupported(f"no initial-events-end bookmark after {idle}s idle")
+        finally:
+            if self.stream is not None:
+                self.stream.close()
+            self.stream = None
+        if errors:
+            st = errors[0]
+            if st.get("code") == 410 or st.get("reason") in ("Expired", "Gone"):
+                raise Expired()
+            raise HttpError(f"watch-list ERROR event: {st.get('message') or st}")
+        if not end:
+            if self._stop.is_set():
+                return
+            raise HttpError("watch-list stream ended before the initial events were complete")
+        self.metrics.c["relists"] += 1
+        self.metrics.c["watch_list_syncs"] += 1
+        read_ns = time.monotonic_ns()
+        ctrl = self.pipeline.reconcile(list(state.values()), read_ns, notify=notify,
+                                       scope_ns=self.namespace if self._scoped() else None)
+        for ev in ctrl:
+            self._handle_control(ev)
+        self.rv = end[0]
+        self.pipeline.last_rv = end[0]
         self.synced.set()
 
     def _scoped(self) -> bool:
@@ -211,7 +320,7 @@ class Reflector:
             try:
                 if need_list:
                     notify = not (first and w.initial_list == "skip")
-                    await self.relist(notify=notify)
+                    await self.sync(notify=notify)
                     need_list = False
                     first = False
                 else:

@@ -90,15 +90,22 @@ class KubeApi:
                          allow_bookmarks: bool = True, label_selector: Optional[str] = None,
                          field_selector: Optional[str] = None,
                          connect_timeout: Optional[float] = None, raw_chunked: bool = False,
-                         on_mode: Optional[Callable[[bool], None]] = None) -> StreamResponse:
+                         on_mode: Optional[Callable[[bool], None]] = None,
+                         send_initial_events: bool = False) -> StreamResponse:
         """Open ``?watch=true``; body bytes go to ``sink(data, read_ns)``.
 
         With ``raw_chunked`` the HTTP chunk framing is left in place for the
         decoder to strip natively; ``on_mode(framed)`` reports which it got.
+        ``send_initial_events`` makes it a WatchList request (streamed initial
+        state ending in a bookmark annotated ``k8s.io/initial-events-end``).
         """
         q: Dict[str, object] = {"watch": "true"}
         if resource_version:
             q["resourceVersion"] = resource_version
+        if send_initial_events:
+            q["sendInitialEvents"] = "true"
+            q["resourceVersionMatch"] = "NotOlderThan"
+            allow_bookmarks = True  # required by the API server for WatchList
         if allow_bookmarks:
             q["allowWatchBookmarks"] = "true"
         if timeout_seconds:

@@ -40,6 +40,7 @@ COUNTERS = (
     "spool_dropped",
     "watch_restarts",
     "relists",
+    "watch_list_syncs",     # initial state via WatchList (sendInitialEvents) instead of LIST
     "expired_410",
     "checkpoints_written",
     "leader_acquired",      # leadership terms started (engine/leader.py)

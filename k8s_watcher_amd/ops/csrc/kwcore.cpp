@@ -827,6 +827,23 @@ void build_core(std::string& o, const PodSpans& S, const std::string& env_json) 
 // ----------------------------------------------------------------------------- Python glue
 
 PyObject* g_json_loads = nullptr;
+// WatchList (sendInitialEvents=true): the BOOKMARK that ends the initial
+// state carries metadata.annotations["k8s.io/initial-events-end"] == "true".
+bool initial_events_end(const Span& annotations) {
+    if (!annotations.present() || annotations.n < 2 || annotations.p[0] != '{') return false;
+    bool found = false;
+    try {
+        Parser P(annotations.p, annotations.p + annotations.n);
+        P.object([&](const char* k, size_t kn) {
+            Span v = P.value();
+            if (KEYIS("k8s.io/initial-events-end") && v.n == 6 && !std::memcmp(v.p, "\"true\"", 6)) found = true;
+        });
+    } catch (const ParseError&) {
+        return false;
+    }
+    return found;
+}
+
 PyObject* g_types[6];  // ADDED MODIFIED DELETED BOOKMARK ERROR INVALID
 enum { T_ADDED, T_MODIFIED, T_DELETED, T_BOOKMARK, T_ERROR, T_INVALID };
 
@@ -1027,6 +1044,12 @@ PyObject* event_tuple(DecoderObject* self, int tidx, PyObject* type_obj, const S
     if (tidx == T_BOOKMARK || tidx < 0) {
         Py_INCREF(Py_None);
         PyTuple_SET_ITEM(t, 7, Py_None);
+        if (tidx == T_BOOKMARK) {  // extra: True on the WatchList end-of-initial-events marker
+            PyObject* end = initial_events_end(S.annotations) ? Py_True : Py_False;
+            Py_INCREF(end);
+            PyTuple_SET_ITEM(t, 8, end);
+            return t;
+        }
     } else {
         build_core(*self->out, S, *self->env_json);
         PyObject* core = PyBytes_FromStringAndSize(self->out->data(), (Py_ssize_t)self->out->size());

@@ -17,7 +17,8 @@ Event tuple layout (index constants below)::
 
 ``obj`` is the pod dict (Python engine) or the payload core bytes (native);
 call ``decoder.core(ev)`` to get core bytes either way. ``extra`` carries the
-``Status`` dict of an ``ERROR`` event or the error text of an ``INVALID`` line.
+``Status`` dict of an ``ERROR`` event, the error text of an ``INVALID`` line,
+or — on a ``BOOKMARK`` — whether it ends a WatchList's initial events.
 """
 
 from __future__ import annotations
@@ -32,6 +33,9 @@ E_TYPE, E_UID, E_NS, E_NAME, E_RV, E_PHASE, E_HAS_STATUS, E_OBJ, E_EXTRA = range
 ADDED, MODIFIED, DELETED, BOOKMARK, ERROR, INVALID = (
     "ADDED", "MODIFIED", "DELETED", "BOOKMARK", "ERROR", "INVALID")
 
+# WatchList (``sendInitialEvents=true``): annotation on the BOOKMARK that ends the initial state
+INITIAL_EVENTS_END = "k8s.io/initial-events-end"
+
 
 def _s(v: Any) -> Optional[str]:
     """Identity fields are strings; anything else (null, numbers) reads as None."""
@@ -43,9 +47,13 @@ def event_from_object(etype: str, obj: Dict[str, Any]) -> tuple:
         return (ERROR, None, None, None, None, None, False, None, obj)
     md = obj.get("metadata") or {}
     st = obj.get("status")
+    extra = None
+    if etype == BOOKMARK:  # True on the WatchList end-of-initial-events marker
+        ann = md.get("annotations")
+        extra = isinstance(ann, dict) and ann.get(INITIAL_EVENTS_END) == "true"
     return (etype, _s(md.get("uid")), _s(md.get("namespace")), _s(md.get("name")),
             _s(md.get("resourceVersion")), _s(st.get("phase")) if st is not None else None,
-            st is not None, obj, None)
+            st is not None, obj, extra)
 
 
 class PyDecoder:

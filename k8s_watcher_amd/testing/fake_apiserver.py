@@ -14,6 +14,8 @@ be faithful where the watcher's correctness depends on it:
   the retained history after it; a compacted version → ``ERROR`` 410 event (or
   HTTP 410 with ``expired_as_http_status``); ``timeoutSeconds``;
   ``allowWatchBookmarks`` bookmarks on demand or periodically;
+* WatchList (``sendInitialEvents=true``): initial state as ``ADDED`` events
+  closed by a bookmark annotated ``k8s.io/initial-events-end``;
 * ``coordination.k8s.io/v1`` Leases (GET/POST/PUT/DELETE, compare-and-swap on
   ``resourceVersion``) for leader election;
 * one HTTP chunk per event, as the real server flushes;
@@ -129,8 +131,10 @@ class _Watch:
 class FakeApiServer:
     def __init__(self, token: Optional[str] = None, history_limit: int = 1_000_000,
                  namespaces: Optional[List[str]] = None, expired_as_http_status: bool = False,
-                 bookmark_interval: Optional[float] = None, start_rv: int = 1000) -> None:
+                 bookmark_interval: Optional[float] = None, start_rv: int = 1000,
+                 watch_list: bool = True) -> None:
         self.token = token
+        self.watch_list = watch_list  # serve sendInitialEvents=true (WatchList)
         self.history_limit = history_limit
         self.extra_namespaces = list(namespaces or ["default", "kube-system"])
         self.expired_as_http_status = expired_as_http_status
@@ -458,6 +462,9 @@ class FakeApiServer:
         w = _Watch(writer, ns, q.get("labelSelector"), q.get("fieldSelector"),
                    q.get("allowWatchBookmarks") in ("true", "1"))
         rv_param = q.get("resourceVersion")
+        if q.get("sendInitialEvents") in ("true", "1"):
+            await self._watch_list(writer, w, q)
+            return
         if rv_param not in (None, "", "0"):
             try:
                 since = int(rv_param)
@@ -484,6 +491,37 @@ class FakeApiServer:
                      b"Transfer-Encoding: chunked\r\n\r\n")
         for line in backlog:
             writer.write(_chunk(line))
+        await self._serve_watch(writer, w, q)
+
+    async def _watch_list(self, writer, w: "_Watch", q: Dict[str, str]) -> None:
+        """WatchList: ADDED for the current state, a bookmark annotated
+        ``k8s.io/initial-events-end``, then live events. Like the real server it
+        requires ``resourceVersionMatch=NotOlderThan`` and bookmarks, and is
+        refused (422) when ``watch_list`` support is off."""
+        if not self.watch_list:
+            self._send_json(writer, 422, _status(422, "Invalid", "sendInitialEvents is forbidden for watch "
+                                                               "unless the WatchList feature gate is enabled"),
+                            "Unprocessable Entity")
+            await writer.drain()
+            return
+        if q.get("resourceVersionMatch") != "NotOlderThan" or not w.bookmarks:
+            self._send_json(writer, 422, _status(422, "Invalid", "sendInitialEvents requires "
+                                                               "resourceVersionMatch=NotOlderThan and "
+                                                               "allowWatchBookmarks=true"), "Unprocessable Entity")
+            await writer.drain()
+            return
+        writer.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\n"
+                     b"Transfer-Encoding: chunked\r\n\r\n")
+        for _, p in sorted(self.pods.items()):
+            if w.wants(p):
+                writer.write(_chunk(json.dumps({"type": "ADDED", "object": p}, separators=(",", ":"),
+                                               ensure_ascii=False).encode() + b"\n"))
+        end = {"type": "BOOKMARK", "object": {"kind": "Pod", "apiVersion": "v1", "metadata": {
+            "resourceVersion": str(self.rv), "annotations": {"k8s.io/initial-events-end": "true"}}}}
+        writer.write(_chunk(json.dumps(end, separators=(",", ":")).encode() + b"\n"))
+        await self._serve_watch(writer, w, q)
+
+    async def _serve_watch(self, writer, w: "_Watch", q: Dict[str, str]) -> None:
         self.watches.add(w)
         timeout = q.get("timeoutSeconds")
         try:

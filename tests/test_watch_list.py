@@ -1,0 +1,106 @@
+"""WatchList initial sync (``watcher.initial_sync: watch_list``, engine/reflector.py).
+
+Not in the reference, whose library LISTs implicitly; the
+streamed form (``sendInitialEvents=true``) must give exactly the LIST result —
+same notifications, same reconcile against the cache — and fall back to LIST
+on API servers without it.
+"""
+
+import asyncio
+
+import pytest
+
+from conftest import run
+from k8s_watcher_amd.testing.podgen import PodFactory
+from test_e2e_slice import check_schema, start_stack
+
+WL = {"watcher": {"initial_sync": "watch_list", "watch_list_idle_seconds": 0.5}}
+
+
+@pytest.mark.parametrize("engine", ["native", "python"])
+def test_watch_list_initial_state_then_live(engine):
+    async def body():
+        f = PodFactory(seed=21, namespaces=["default", "kube-system", "batch"])
+        pods = [f.running(f.new_pod()) for _ in range(12)]
+        srv, sink, svc = await start_stack("development", overrides=WL, engine=engine, pods=pods)
+        await svc.start()
+        want = [p for p in pods if p["metadata"]["namespace"] in ("default", "kube-system")]
+        await sink.state.wait_for(len(want), timeout=10)
+        assert svc.metrics.c["watch_list_syncs"] == 1
+        await asyncio.wait_for(svc.reflectors[0].connected.wait(), 5)
+        watch_reqs = [t for _, t in srv.requests if "watch=true" in t]
+        assert "sendInitialEvents=true" in watch_reqs[0] and "resourceVersionMatch=NotOlderThan" in watch_reqs[0]
+        assert not any("watch" not in t and "/pods" in t for _, t in srv.requests)  # no LIST
+        # after the initial-events-end bookmark the regular watch resumes from its RV
+        assert "sendInitialEvents" not in watch_reqs[-1] and "resourceVersion=" in watch_reqs[-1]
+        p = f.running(f.new_pod("default"))
+        srv.create(p)
+        await sink.state.wait_for(len(want) + 1, timeout=10)
+        got = sink.state.payloads()
+        for g in got:
+            check_schema(g, "development")
+        assert sorted(g["uid"] for g in got) == sorted([x["metadata"]["uid"] for x in want] + [p["metadata"]["uid"]])
+        svc.stop()
+        await svc.shutdown()
+        await sink.stop()
+        await srv.stop()
+    run(body())
+
+
+@pytest.mark.parametrize("support", ["refused", "ignored"])
+def test_watch_list_falls_back_to_list(support, monkeypatch):
+    async def body():
+        f = PodFactory(seed=22, namespaces=["default"])
+        pods = [f.running(f.new_pod()) for _ in range(4)]
+        srv, sink, svc = await start_stack("staging", overrides=WL, pods=pods,
+                                           server_kwargs={"watch_list": support != "refused"})
+        if support == "ignored":
+            # an API server that predates WatchList: the parameter is silently ignored
+            orig = srv._watch
+
+            async def no_watch_list(writer, ns, q):
+                q = {k: v for k, v in q.items() if k not in ("sendInitialEvents", "resourceVersionMatch")}
+                await orig(writer, ns, q)
+            monkeypatch.setattr(srv, "_watch", no_watch_list)
+        await svc.start()
+        await sink.state.wait_for(4, timeout=10)
+        await asyncio.sleep(0.2)
+        assert svc.metrics.c["watch_list_syncs"] == 0 and svc.metrics.c["relists"] == 1
+        assert svc.reflectors[0].watch_list is False
+        uids = [g["uid"] for g in sink.state.payloads()]
+        assert sorted(set(uids)) == sorted(p["metadata"]["uid"] for p in pods)
+        svc.stop()
+        await svc.shutdown()
+        await sink.stop()
+        await srv.stop()
+    run(body())
+
+
+def test_watch_list_after_410_reconciles_like_relist():
+    async def body():
+        f = PodFactory(seed=23, namespaces=["default"])
+        pods = [f.running(f.new_pod()) for _ in range(5)]
+        srv, sink, svc = await start_stack("staging", overrides=WL, pods=pods)
+        await svc.start()
+        await sink.state.wait_for(5, timeout=10)
+        # while the watch is down: one pod deleted, one modified, one added, then history compacted
+        srv.drop_connections()
+        srv.delete("default", pods[0]["metadata"]["name"])
+        changed = dict(pods[1])
+        changed["status"] = dict(changed["status"], phase="Succeeded")
+        srv.update(changed)
+        added = f.running(f.new_pod("default"))
+        srv.create(added)
+        srv.compact()
+        await sink.state.wait_for(8, timeout=10)
+        await asyncio.sleep(0.3)
+        tail = [(g["event_type"], g["uid"]) for g in sink.state.payloads()[5:]]
+        assert sorted(tail) == sorted([("DELETED", pods[0]["metadata"]["uid"]),
+                                       ("MODIFIED", pods[1]["metadata"]["uid"]),
+                                       ("ADDED", added["metadata"]["uid"])])
+        assert svc.metrics.c["watch_list_syncs"] == 2 and svc.metrics.c["expired_410"] >= 1
+        svc.stop()
+        await svc.shutdown()
+        await sink.stop()
+        await srv.stop()
+    run(body())
