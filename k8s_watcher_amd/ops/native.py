@@ -33,11 +33,43 @@ def compiler() -> str:
     raise NativeUnavailable("no C++ compiler found (set $CXX)")
 
 
-def build_command() -> list:
+SANITIZERS = {
+    # host-code sanitizers for tests (scripts/sanitize.sh); never the production build
+    "address": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"],
+    "thread": ["-fsanitize=thread"],
+}
+
+
+def build_command(sanitize: str = "", out: str = SO) -> list:
     inc = sysconfig.get_paths()["include"]
-    return [compiler(), "-O3", "-std=c++17", "-pthread", "-fPIC", "-shared", "-fvisibility=hidden",
+    opt = ["-O1", "-g"] + SANITIZERS[sanitize] if sanitize else ["-O3"]
+    return [compiler(), *opt, "-std=c++17", "-pthread", "-fPIC", "-shared", "-fvisibility=hidden",
             "-fno-strict-aliasing", "-Wall", "-Wno-shadow", "-Wno-unused-function", "-Wno-psabi",
-            f"-I{inc}", f"-I{os.path.dirname(SRC)}", SRC, "-o", SO]
+            f"-I{inc}", f"-I{os.path.dirname(SRC)}", SRC, "-o", out]
+
+
+def sanitizer_so(kind: str) -> str:
+    """Path of the sanitizer build of the extension (outside the package: never imported by default)."""
+    root = os.path.dirname(os.path.dirname(HERE))
+    return os.path.join(root, "build", f"sanitize-{kind}", os.path.basename(SO))
+
+
+def build_sanitized(kind: str, quiet: bool = False) -> str:
+    """Compile ``_kwcore`` with ``-fsanitize=<kind>`` into ``build/sanitize-<kind>/``.
+
+    Load it with ``$K8S_WATCHER_KWCORE_SO=<path>`` and the matching runtime in
+    ``LD_PRELOAD`` (the interpreter itself is not instrumented).
+    """
+    out = sanitizer_so(kind)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = build_command(kind, out + ".tmp")
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise NativeUnavailable(f"building sanitized _kwcore failed:\n{' '.join(cmd)}\n{res.stderr}")
+    os.replace(out + ".tmp", out)
+    if not quiet:
+        print(f"built {out}")
+    return out
 
 
 def sources() -> list:
@@ -74,6 +106,17 @@ _mod = None
 def load():
     global _mod
     if _mod is None:
+        override = os.environ.get("K8S_WATCHER_KWCORE_SO")
+        if override:  # a sanitizer build (build_sanitized); tests only
+            import importlib.util
+            spec = importlib.util.spec_from_file_location("k8s_watcher_amd.ops._kwcore", override)
+            if spec is None or spec.loader is None:
+                raise NativeUnavailable(f"cannot load {override}")
+            mod = importlib.util.module_from_spec(spec)
+            sys.modules["k8s_watcher_amd.ops._kwcore"] = mod
+            spec.loader.exec_module(mod)
+            _mod = mod
+            return _mod
         try:
             _mod = importlib.import_module("k8s_watcher_amd.ops._kwcore")
         except ImportError as exc:
@@ -114,6 +157,9 @@ class NativeDecoder:
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] in SANITIZERS:
+        build_sanitized(sys.argv[1])
+        sys.exit(0)
     build(quiet=False)
     mod = load()
     print("loaded", mod.__file__, mod.cpu_features())
