@@ -199,3 +199,32 @@ def test_two_replicas_leader_election_cli(cluster):
     assert b.returncode == 0, err_b
     assert "Acquired leadership of lease default/k8s-watcher-amd as replica-b" in err_b
     assert err_b.count("Pod event detected: ADDED - default/") == 3
+
+
+def test_podwatcher_subclass_hooks_run_per_event(cluster):
+    """A reference user's subclass overriding handle_pod_event keeps working:
+    start_watching hands every event to the override (pod_watcher.py:266-269)."""
+    import threading
+    from watcher.pod_watcher import PodWatcher
+    st, srv, cfg = cluster
+    seen = []
+
+    class Mine(PodWatcher):
+        def handle_pod_event(self, event_type, pod):
+            seen.append((event_type, pod.metadata.namespace, pod.metadata.name))
+            if len(seen) == 4:
+                self.watch.stop()  # ends the stream after this event
+            return super().handle_pod_event(event_type, pod)
+
+    w = Mine("staging", config_dir=cfg)
+    assert w._customised() and not PodWatcher("staging", config_dir=cfg)._customised()
+    t = threading.Thread(target=w.start_watching, daemon=True)
+    t.start()
+    deadline = time.time() + 20
+    while len(seen) < 3 and time.time() < deadline:
+        time.sleep(0.05)
+    assert [s[0] for s in seen] == ["ADDED"] * 3
+    f = PodFactory(seed=9, namespaces=["default"])
+    st.call(srv.create, f.running(f.new_pod()))
+    t.join(20)
+    assert not t.is_alive() and len(seen) == 4 and seen[3][0] == "ADDED"

@@ -131,8 +131,25 @@ class PodWatcher:
         return data
 
     # ------------------------------------------------------------------ run
+    def _customised(self) -> bool:
+        """True when a subclass overrides a per-event hook of the reference API."""
+        cls = type(self)
+        return any(getattr(cls, m) is not getattr(PodWatcher, m)
+                   for m in ("handle_pod_event", "should_process_event", "_extract_pod_data"))
+
     def start_watching(self) -> None:
-        """Run the asynchronous engine until SIGINT/SIGTERM or a fatal watch error."""
+        """Run until SIGINT/SIGTERM or a fatal watch error.
+
+        The stock class runs the asynchronous engine (:class:`WatcherService`).
+        A subclass that overrides ``handle_pod_event``, ``should_process_event``
+        or ``_extract_pod_data`` gets the reference's own loop instead
+        (``pod_watcher.py:243-277``): every watch event is handed to
+        ``self.handle_pod_event(type, pod)``, so the overrides run exactly as
+        they did on the reference.
+        """
+        if self._customised():
+            self._start_watching_per_event()
+            return
         from k8s_watcher_amd.engine.service import SetupError, WatcherService
 
         async def run() -> None:
@@ -151,3 +168,28 @@ class PodWatcher:
             raise
         except KeyboardInterrupt:
             logging.getLogger("watcher.pod_watcher").info("Stopping Pod watcher...")
+
+    def _start_watching_per_event(self) -> None:
+        """The reference's synchronous loop over the compat ``Watch`` (``pod_watcher.py:243-277``),
+        with its fixes: setup failure raises (exit 1) and the notifier is attached when enabled."""
+        from k8s_watcher_amd.engine.service import SetupError
+        if not self.setup_k8s_client():
+            self.logger.error("Failed to setup Kubernetes client")
+            raise SetupError("Failed to setup Kubernetes client")
+        if self.settings.clusterapi.enabled and self.clusterapi_client is None:
+            self.clusterapi_client = self._setup_clusterapi_client()
+        self.logger.info(f"Starting Pod watcher in {self.environment} environment...")
+        if self.settings.watcher.namespaces:
+            self.logger.info(f"Monitoring namespaces: {self.settings.watcher.namespaces}")
+        else:
+            self.logger.info("Monitoring all namespaces")
+        try:
+            for event in self.watch.stream(self.v1.list_pod_for_all_namespaces):
+                self.handle_pod_event(event["type"], event["object"])
+        except KeyboardInterrupt:
+            self.logger.info("Stopping Pod watcher...")
+        except Exception as exc:
+            self.logger.error(f"Error in Pod watcher: {exc}")
+            raise
+        finally:
+            self.watch.stop()
