@@ -11,6 +11,7 @@ silently falling back to the Python engine.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
 import shutil
 import subprocess
@@ -108,7 +109,6 @@ def load():
     if _mod is None:
         override = os.environ.get("K8S_WATCHER_KWCORE_SO")
         if override:  # a sanitizer build (build_sanitized); tests only
-            import importlib.util
             spec = importlib.util.spec_from_file_location("k8s_watcher_amd.ops._kwcore", override)
             if spec is None or spec.loader is None:
                 raise NativeUnavailable(f"cannot load {override}")
