@@ -95,7 +95,8 @@ class WatcherService:
         try:
             ep = self.load_endpoint()
             self.endpoint = ep
-            self.api = KubeApi(ep, timeout=self.settings.kubernetes.request_timeout)
+            self.api = KubeApi(ep, timeout=self.settings.kubernetes.request_timeout,
+                               compression=self.settings.kubernetes.compression)
             ver = await self.api.get_version()
             self.server_version = ver.get("gitVersion") or f"{ver.get('major')}.{ver.get('minor')}"
             self.log.info(f"Successfully connected to Kubernetes API version: {self.server_version}")

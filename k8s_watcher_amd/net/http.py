@@ -19,6 +19,7 @@ from __future__ import annotations
 import asyncio
 import ssl as _ssl
 import time
+import zlib
 from typing import Callable, Dict, List, Optional, Tuple
 from urllib.parse import urlencode, urlsplit
 from ..utils.aio import with_timeout
@@ -493,7 +494,14 @@ class HttpClient:
 
             def _done(p: ResponseParser, f=fut) -> None:
                 if not f.done():
-                    f.set_result(Response(p.status, p.reason, p.headers, p.body()))
+                    body = p.body()
+                    if body and p.headers.get("content-encoding", "").lower() == "gzip":
+                        try:
+                            body = zlib.decompress(body, 16 + zlib.MAX_WBITS)
+                        except zlib.error as exc:
+                            f.set_exception(HttpError(f"bad gzip response body: {exc}"))
+                            return
+                    f.set_result(Response(p.status, p.reason, p.headers, body))
 
             proto.parser.on_complete = _done
             assert proto.transport is not None

@@ -34,6 +34,7 @@ import asyncio
 import base64
 import collections
 import copy
+import gzip
 import json
 import threading
 import time
@@ -45,6 +46,7 @@ from ..utils.aio import with_timeout
 JSON = "application/json"
 
 
+GZIP_THRESHOLD = 128 * 1024  # kube-apiserver compresses responses larger than this
 LEASES_PREFIX = "/apis/coordination.k8s.io/v1/namespaces/"
 _REASONS = {200: "OK", 201: "Created", 400: "Bad Request", 404: "Not Found", 405: "Method Not Allowed",
             409: "Conflict", 500: "Internal Server Error", 503: "Service Unavailable"}
@@ -152,6 +154,7 @@ class FakeApiServer:
         self.port = 0
         self.loop: Optional[asyncio.AbstractEventLoop] = None
         self._bm_task: Optional[asyncio.Task] = None
+        self.gzipped_responses = 0
         self.leases: Dict[Tuple[str, str], Dict[str, Any]] = {}
         self.lease_writes: List[Tuple[Tuple[str, str], Dict[str, Any]]] = []
         self.lease_fault: Optional[int] = None  # answer every lease request with this status
@@ -337,10 +340,15 @@ class FakeApiServer:
             except Exception:  # noqa: BLE001
                 pass
 
-    def _send_json(self, writer, code: int, doc: Any, reason: str = "OK") -> None:
+    def _send_json(self, writer, code: int, doc: Any, reason: str = "OK", gzip_ok: bool = False) -> None:
         body = json.dumps(doc, separators=(",", ":"), ensure_ascii=False).encode("utf-8")
-        writer.write(b"HTTP/1.1 %d %s\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n"
-                     % (code, reason.encode(), len(body)) + body)
+        extra = b""
+        if gzip_ok and len(body) > GZIP_THRESHOLD:  # as the API server: only large responses
+            body = gzip.compress(body, compresslevel=1)
+            extra = b"Content-Encoding: gzip\r\n"
+            self.gzipped_responses += 1
+        writer.write(b"HTTP/1.1 %d %s\r\nContent-Type: application/json\r\n%sContent-Length: %d\r\n\r\n"
+                     % (code, reason.encode(), extra, len(body)) + body)
 
     async def _route(self, method: str, target: str, headers: Dict[str, str], writer,
                      body: bytes = b"") -> bool:
@@ -386,7 +394,8 @@ class FakeApiServer:
         pods = [p for (pns, _), p in sorted(self.pods.items())
                 if (ns is None or pns == ns) and _match_labels(p, q.get("labelSelector"))
                 and _match_fields(p, q.get("fieldSelector"))]
-        self._send_json(writer, 200, self._paginate("PodList", pods, q))
+        self._send_json(writer, 200, self._paginate("PodList", pods, q),
+                        gzip_ok="gzip" in headers.get("accept-encoding", ""))
         return True
 
     # ------------------------------------------------------------------ leases

@@ -201,6 +201,7 @@ class KubernetesSettings:
     context: Optional[str] = None
     use_mock: bool = False
     request_timeout: float = 30.0
+    compression: bool = True  # Accept-Encoding: gzip on LIST requests
 
 
 @dataclass
@@ -402,6 +403,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         context=k.get("context") or None,
         use_mock=_as_bool(k.get("use_mock", False), "kubernetes.use_mock"),
         request_timeout=_as_float(k.get("request_timeout", 30.0), "kubernetes.request_timeout"),
+        compression=_as_bool(k.get("compression", True), "kubernetes.compression"),
     )
 
     level = str(w.get("log_level", "INFO")).upper()

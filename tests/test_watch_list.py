@@ -104,3 +104,23 @@ def test_watch_list_after_410_reconciles_like_relist():
         await sink.stop()
         await srv.stop()
     run(body())
+
+
+@pytest.mark.parametrize("compression", [True, False])
+def test_gzip_list(compression):
+    """LIST asks for gzip (``kubernetes.compression``); the fake API server, like the
+    real one, compresses bodies over 128 KiB; the watcher decodes them transparently."""
+    async def body():
+        f = PodFactory(seed=24, namespaces=["default"])
+        pods = [f.running(f.new_pod()) for _ in range(150)]
+        ov = {"kubernetes": {"compression": compression}, "watcher": {"list_page_size": 1000}}
+        srv, sink, svc = await start_stack("staging", overrides=ov, pods=pods)
+        await svc.start()
+        await sink.state.wait_for(150, timeout=10)
+        assert srv.gzipped_responses == (1 if compression else 0)
+        assert sorted(g["uid"] for g in sink.state.payloads()) == sorted(p["metadata"]["uid"] for p in pods)
+        svc.stop()
+        await svc.shutdown()
+        await sink.stop()
+        await srv.stop()
+    run(body())
