@@ -127,8 +127,8 @@ class WatcherService:
         if not c.enabled:
             return NullNotifier(self.metrics)
         log_events = w.log_events if w.log_events is not None else self.log.isEnabledFor(logging.INFO)
-        if w.engine == "native" and c.pool.native and c.base_url.startswith("http://"):
-            # per-request work in C++ (ops/csrc/engine.inc); TLS endpoints use the asyncio pool
+        if w.engine == "native" and c.pool.native:
+            # per-request work in C++ (ops/csrc/engine.inc), TLS included
             return NativeNotifierPool(c, self.metrics, ts_mode=w.event_timestamp, log_events=log_events,
                                       on_saturation=self._on_saturation, event_log=self.event_log)
         return NotifierPool(c, self.metrics, ts_mode=w.event_timestamp, log_events=log_events,

@@ -18,6 +18,11 @@
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 
+#include <arpa/inet.h>
+#include <openssl/err.h>
+#include <openssl/ssl.h>
+#include <openssl/x509v3.h>
+
 #include <linux/futex.h>
 #include <sys/socket.h>
 #include <sys/syscall.h>

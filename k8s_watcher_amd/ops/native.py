@@ -46,7 +46,7 @@ def build_command(sanitize: str = "", out: str = SO) -> list:
     opt = ["-O1", "-g"] + SANITIZERS[sanitize] if sanitize else ["-O3"]
     return [compiler(), *opt, "-std=c++17", "-pthread", "-fPIC", "-shared", "-fvisibility=hidden",
             "-fno-strict-aliasing", "-Wall", "-Wno-shadow", "-Wno-unused-function", "-Wno-psabi",
-            f"-I{inc}", f"-I{os.path.dirname(SRC)}", SRC, "-o", out]
+            f"-I{inc}", f"-I{os.path.dirname(SRC)}", SRC, "-o", out, "-lssl", "-lcrypto"]
 
 
 def sanitizer_so(kind: str) -> str:
@@ -83,9 +83,8 @@ def is_fresh() -> bool:
 
 
 def build(quiet: bool = False) -> str:
-    cmd = build_command()
     tmp = SO + ".tmp"
-    cmd[-1] = tmp
+    cmd = build_command(out=tmp)
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise NativeUnavailable(f"building _kwcore failed:\n{' '.join(cmd)}\n{res.stderr}")

@@ -14,8 +14,10 @@ This wrapper owns the asyncio side only: it connects sockets
 the core's retry decisions into ``call_later`` timers, writes the log lines
 the core reports and feeds its latency samples into :class:`Metrics`.
 
-Plain HTTP only: for an ``https`` clusterapi the service uses the asyncio
-pool, whose transports do TLS.
+For an ``https`` clusterapi the core also runs TLS (OpenSSL, non-blocking,
+handshake driven by socket readiness; certificate and hostname/IP checks
+per ``clusterapi.verify_tls`` / ``ca_file``), so the production profile's
+https endpoint gets the same per-request path.
 """
 
 from __future__ import annotations
@@ -45,8 +47,9 @@ class NativeNotifierPool:
                  on_saturation: Optional[Callable[[bool], None]] = None,
                  event_log: Optional[EventLog] = None, **_ignored) -> None:
         u = urlsplit(settings.base_url)
-        if u.scheme != "http":
-            raise ValueError("NativeNotifierPool supports plain http clusterapi URLs only")
+        if u.scheme not in ("http", "https"):
+            raise ValueError(f"unsupported clusterapi URL scheme in {settings.base_url!r}")
+        self.tls = u.scheme == "https"
         self.settings = settings
         self.metrics = metrics or Metrics()
         self.loop = asyncio.get_running_loop()
@@ -55,10 +58,11 @@ class NativeNotifierPool:
         self.elog = event_log if event_log is not None else EventLog(self.svc_log)
         self.log_events = log_events
         self.host = u.hostname or "localhost"
-        self.port = u.port or 80
+        default_port = 443 if self.tls else 80
+        self.port = u.port or default_port
         self.endpoint_url = settings.base_url + settings.pod_update
         path = (u.path.rstrip("/") + settings.pod_update) or "/"
-        host_hdr = self.host if self.port == 80 else f"{self.host}:{self.port}"
+        host_hdr = self.host if self.port == default_port else f"{self.host}:{self.port}"
         head = (f"POST {path} HTTP/1.1\r\nHost: {host_hdr}\r\nContent-Type: application/json\r\n"
                 f"User-Agent: k8s-watcher-amd/1.0\r\n")
         if settings.api_key:
@@ -69,6 +73,8 @@ class NativeNotifierPool:
             head.encode("latin-1"), settings.pool.connections, settings.pool.pipeline_depth, r.max_attempts,
             r.delay_seconds, r.multiplier, r.max_delay_seconds, settings.pool.coalesce, log_events,
             sorted(RETRYABLE_STATUS), self.metrics.c)
+        if self.tls:  # TLS runs inside the core (OpenSSL on the same non-blocking sockets)
+            self.core.enable_tls(self.host, settings.ca_file, settings.verify_tls)
         self.n = settings.pool.connections
         self.socks: Dict[int, socket.socket] = {}
         self.connecting: set = set()
@@ -122,13 +128,23 @@ class NativeNotifierPool:
         return self.core.pending()
 
     async def health_check(self, timeout: float = 5.0) -> bool:
-        client = HttpClient(self.settings.base_url, timeout=timeout)
+        client = HttpClient(self.settings.base_url, self._health_ssl_context(), timeout=timeout)
         try:
             return (await client.request("GET", self.settings.health)).ok
         except Exception:  # noqa: BLE001 - parity: any failure -> False
             return False
         finally:
             await client.close()
+
+    def _health_ssl_context(self):
+        if not self.tls:
+            return None
+        import ssl
+        ctx = ssl.create_default_context(cafile=self.settings.ca_file)
+        if not self.settings.verify_tls:
+            ctx.check_hostname = False
+            ctx.verify_mode = ssl.CERT_NONE
+        return ctx
 
     async def warm_up(self, timeout: float = 2.0) -> int:
         await asyncio.gather(*[self._connect(i) for i in range(self.n) if i not in self.socks],

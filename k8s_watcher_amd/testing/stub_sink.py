@@ -181,19 +181,20 @@ class StubSink:
         self.port = 0
 
     async def start(self, host: str = "127.0.0.1", port: int = 0, reuse_port: bool = False,
-                    sock: Optional[socket.socket] = None) -> int:
+                    sock: Optional[socket.socket] = None, ssl_context=None) -> int:
         loop = asyncio.get_running_loop()
+        self.scheme = "https" if ssl_context is not None else "http"
         if sock is not None:
-            self.server = await loop.create_server(lambda: _SinkProtocol(self.state), sock=sock)
+            self.server = await loop.create_server(lambda: _SinkProtocol(self.state), sock=sock, ssl=ssl_context)
         else:
             self.server = await loop.create_server(lambda: _SinkProtocol(self.state), host, port,
-                                                   reuse_port=reuse_port or None)
+                                                   reuse_port=reuse_port or None, ssl=ssl_context)
         self.port = self.server.sockets[0].getsockname()[1]
         return self.port
 
     @property
     def url(self) -> str:
-        return f"http://127.0.0.1:{self.port}"
+        return f"{getattr(self, 'scheme', 'http')}://127.0.0.1:{self.port}"
 
     async def stop(self) -> None:
         if self.server is not None:
