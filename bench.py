@@ -64,6 +64,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-placement", dest="placement", action="store_false",
                     help="no per-rank L3 domain assignment (each watcher still pins per watcher.decode_affinity)")
     ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
+    ap.add_argument("--tls", action="store_true",
+                    help="https clusterapi (as production.yaml): the stub sink serves TLS with a throw-away CA")
     ap.add_argument("--sink-workers", type=int, default=4)
     ap.add_argument("--latency-rate", type=float, default=100.0)
     ap.add_argument("--latency-seconds", type=float, default=3.0)
@@ -168,8 +170,15 @@ async def rank_main(args, d: Dist) -> dict:
                          "--pods-per-step", str(args.pods_per_step), "--seed", str(d.rank),
                          "--prerender", str(args.warmup + args.steps))
     sink_port = free_port()
+    tls_args, pki = [], None
+    if args.tls:
+        import tempfile
+        from k8s_watcher_amd.testing.certs import make_pki
+        pki = make_pki(tempfile.mkdtemp(prefix="bench-pki-"))
+        tls_args = ["--tls-cert", pki.server_crt, "--tls-key", pki.server_key]
+    scheme = "https" if args.tls else "http"
     sink = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.stub_sink", "--port", str(sink_port),
-                       "--workers", str(args.sink_workers))
+                       "--workers", str(args.sink_workers), *tls_args)
     try:
         ready = (await asyncio.wait_for(replay.stdout.readline(), 600)).decode().split()
         assert ready and ready[0] == "READY", ready
@@ -186,7 +195,8 @@ async def rank_main(args, d: Dist) -> dict:
         log_path = os.path.join("/tmp", f"k8s-watcher-bench-{os.getpid()}.log")
         setup_logging(args.profile, "WARNING" if args.profile == "production" else "INFO", log_file=log_path)
         overrides = {
-            "clusterapi": {"base_url": f"http://127.0.0.1:{sink_port}", "timeout": 30,
+            "clusterapi": {"base_url": f"{scheme}://127.0.0.1:{sink_port}", "timeout": 30,
+                           **({"ca_file": pki.ca_crt} if pki else {}),
                            "enabled": not os.environ.get("BENCH_NO_NOTIFY")},
             "watcher": {"engine": args.engine, "retry": {"max_attempts": 0, "delay_seconds": 0.05},
                         **({"decode_threads": args.decode_threads} if args.decode_threads is not None else {}),
@@ -268,7 +278,8 @@ async def rank_main(args, d: Dist) -> dict:
 
         ref = None
         if args.ref_events > 0 and d.rank == 0:
-            ref = await run_reference(args, api_port, sink_port, cmd, args.warmup + args.steps + 1)
+            ref = await run_reference(args, api_port, f"{scheme}://127.0.0.1:{sink_port}", cmd,
+                                      args.warmup + args.steps + 1, pki.ca_crt if pki else None)
         replay.stdin.write(b"QUIT\n")
         await replay.stdin.drain()
         return {"elapsed": elapsed, "events": events, "notified": notified, "events_per_step": events_per_step,
@@ -319,13 +330,13 @@ def cpu_snapshot(replay_pid: int, sink_pid: int) -> dict:
     return {"watcher": t.user + t.system, "replay": tree(replay_pid), "sink": tree(sink_pid)}
 
 
-async def run_reference(args, api_port: int, sink_port: int, cmd, step: int) -> dict:
+async def run_reference(args, api_port: int, sink_url: str, cmd, step: int, ca_file=None) -> dict:
     from benchmarks.reference_equiv import RefEquivWatcher
     from k8s_watcher_amd.utils.config import load_settings
 
     s = load_settings(args.profile)
     ref = RefEquivWatcher(args.profile, s.watcher.namespaces, s.watcher.critical_events_only,
-                          f"http://127.0.0.1:{sink_port}")
+                          sink_url, ca_file=ca_file)
     loop = asyncio.get_running_loop()
     connected = loop.create_future()
     result = {}
@@ -392,6 +403,7 @@ def main(argv=None) -> int:
             "parallelism": f"shard{d.world}" if d.world > 1 else "single-process",
             "engine": args.engine,
             "decode_threads": res["decode_threads"],
+            "clusterapi": "https" if args.tls else "http",
         },
         "p50_latency_ms": round(p50 / 1e6, 3) if p50 else None,
         "p99_latency_ms": round(p99 / 1e6, 3) if p99 else None,

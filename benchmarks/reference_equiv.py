@@ -64,11 +64,14 @@ def _convert(key: str, v: Any) -> Any:
 
 class RefEquivWatcher:
     def __init__(self, environment: str, namespaces, critical_events_only: bool, sink_url: str,
-                 logger: Optional[logging.Logger] = None) -> None:
+                 logger: Optional[logging.Logger] = None, ca_file: Optional[str] = None) -> None:
         self.environment = environment
         self.namespaces = list(namespaces or [])
         self.critical = environment == "production" and critical_events_only
         self.session = requests.Session()
+        # https clusterapi (bench --tls): verify against the test CA (per request:
+        # a session-level verify loses to $REQUESTS_CA_BUNDLE in requests)
+        self.post_kw = {"verify": ca_file} if ca_file else {}
         self.endpoint = sink_url.rstrip("/") + "/api/pods/update"
         self.logger = logger or logging.getLogger("watcher.pod_watcher")
         self.processed = 0
@@ -123,7 +126,7 @@ class RefEquivWatcher:
             return
         data = self.extract_pod_data(pod)
         data["event_type"] = event_type
-        resp = self.session.post(self.endpoint, json=data)
+        resp = self.session.post(self.endpoint, json=data, **self.post_kw)
         if resp.status_code == 200:
             self.notified += 1
             self.latencies_ns.append(time.monotonic_ns() - read_ns)

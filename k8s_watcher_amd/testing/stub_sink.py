@@ -232,7 +232,7 @@ class _VerifyingState(SinkState):
 
 
 def run_sink_process(port: int, workers: int = 1, latency: float = 0.0,
-                     verify_dir: Optional[str] = None) -> None:
+                     verify_dir: Optional[str] = None, tls: Optional[Tuple[str, str]] = None) -> None:
     """Blocking: serve on ``port`` with ``workers`` SO_REUSEPORT processes (bench helper).
 
     With ``verify_dir`` every worker records ``uid|event_type|phase`` counts and
@@ -251,7 +251,12 @@ def run_sink_process(port: int, workers: int = 1, latency: float = 0.0,
         sink = StubSink(record=False, latency=latency)
         if verify_dir:
             sink.state = _VerifyingState(latency=latency)
-        await sink.start("127.0.0.1", port, reuse_port=True)
+        ctx = None
+        if tls:
+            import ssl
+            ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+            ctx.load_cert_chain(*tls)
+        await sink.start("127.0.0.1", port, reuse_port=True, ssl_context=ctx)
         stop = asyncio.Event()
         loop = asyncio.get_running_loop()
         loop.add_signal_handler(_signal.SIGTERM, stop.set)
@@ -273,9 +278,12 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--workers", type=int, default=1)
     ap.add_argument("--latency", type=float, default=0.0)
     ap.add_argument("--verify-dir", default=None, help="record payload keys, dump on SIGTERM")
+    ap.add_argument("--tls-cert", default=None, help="serve https with this certificate (and --tls-key)")
+    ap.add_argument("--tls-key", default=None)
     args = ap.parse_args(argv)
-    print(f"stub clusterapi listening on http://127.0.0.1:{args.port}", flush=True)
-    run_sink_process(args.port, args.workers, args.latency, args.verify_dir)
+    tls = (args.tls_cert, args.tls_key) if args.tls_cert else None
+    print(f"stub clusterapi listening on {'https' if tls else 'http'}://127.0.0.1:{args.port}", flush=True)
+    run_sink_process(args.port, args.workers, args.latency, args.verify_dir, tls)
 
 
 if __name__ == "__main__":
