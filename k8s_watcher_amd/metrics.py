@@ -78,6 +78,19 @@ class LatencyHistogram:
         if self.samples is not None:
             self.samples.extend(values)
 
+    def add_counts(self, counts: "array.array", total_ns: int, n: int) -> None:
+        """Merge bucket counts computed elsewhere (the native notifier core)."""
+        c = self.counts
+        for i, v in enumerate(counts):
+            if v:
+                c[i] += v
+        self.total_ns += total_ns
+        self.n += n
+
+    def add_samples(self, values: "array.array") -> None:
+        if self.samples is not None:
+            self.samples.extend(values)
+
     def reset(self) -> None:
         self.counts = [0] * (len(_BUCKETS_NS) + 1)
         self.total_ns = 0
@@ -105,7 +118,9 @@ class LatencyHistogram:
 class Metrics:
     def __init__(self, record_samples: bool = False) -> None:
         self.c: Dict[str, int] = {k: 0 for k in COUNTERS}
-        self.latency = LatencyHistogram(record_samples)
+        self.latency = LatencyHistogram(record_samples)  # socket read of the event -> 2xx from clusterapi
+        self.rtt = LatencyHistogram()  # request on the wire -> 2xx (clusterapi + network share)
+        self.record_samples = record_samples
         self.started = time.time()
         self.ready = False
         self.gauges: Dict[str, Callable[[], float]] = {}
@@ -133,16 +148,16 @@ class Metrics:
             name = f"k8s_watcher_{k}"
             lines.append(f"# TYPE {name} gauge")
             lines.append(f"{name} {fn()}")
-        h = self.latency
-        name = "k8s_watcher_notify_latency_seconds"
-        lines.append(f"# TYPE {name} histogram")
-        acc = 0
-        for ub, c in zip(_BUCKETS_NS, h.counts):
-            acc += c
-            lines.append(f'{name}_bucket{{le="{ub / 1e9:.9g}"}} {acc}')
-        lines.append(f'{name}_bucket{{le="+Inf"}} {h.n}')
-        lines.append(f"{name}_sum {h.total_ns / 1e9:.9f}")
-        lines.append(f"{name}_count {h.n}")
+        for name, h in (("k8s_watcher_notify_latency_seconds", self.latency),
+                        ("k8s_watcher_notify_rtt_seconds", self.rtt)):
+            lines.append(f"# TYPE {name} histogram")
+            acc = 0
+            for ub, c in zip(_BUCKETS_NS, h.counts):
+                acc += c
+                lines.append(f'{name}_bucket{{le="{ub / 1e9:.9g}"}} {acc}')
+            lines.append(f'{name}_bucket{{le="+Inf"}} {h.n}')
+            lines.append(f"{name}_sum {h.total_ns / 1e9:.9f}")
+            lines.append(f"{name}_count {h.n}")
         return "\n".join(lines) + "\n"
 
 

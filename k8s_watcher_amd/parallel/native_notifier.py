@@ -30,7 +30,7 @@ import time
 from typing import Callable, Dict, Optional
 from urllib.parse import urlsplit
 
-from ..metrics import Metrics
+from ..metrics import _BUCKETS_NS, Metrics
 from ..net.http import HttpClient
 from ..ops.native import load
 from ..utils.aio import with_timeout
@@ -73,6 +73,8 @@ class NativeNotifierPool:
             head.encode("latin-1"), settings.pool.connections, settings.pool.pipeline_depth, r.max_attempts,
             r.delay_seconds, r.multiplier, r.max_delay_seconds, settings.pool.coalesce, log_events,
             sorted(RETRYABLE_STATUS), self.metrics.c)
+        # histograms accumulate in C++; raw samples only when the Metrics keep them (benchmarks)
+        self.core.set_histograms(_BUCKETS_NS, self.metrics.record_samples)
         if self.tls:  # TLS runs inside the core (OpenSSL on the same non-blocking sockets)
             self.core.enable_tls(self.host, settings.ca_file, settings.verify_tls)
         self.n = settings.pool.connections
@@ -249,7 +251,7 @@ class NativeNotifierPool:
         self._after()
 
     def _after(self, connect_failed: Optional[int] = None) -> None:
-        retries, logs, need_connect, want_write, lost, lat, spooled = self.core.take()
+        retries, logs, need_connect, want_write, lost, lat, spooled, hist = self.core.take()
         if spooled:
             for uid in self.spool.append(spooled):
                 self.core.spool_watch(uid, True)
@@ -267,8 +269,12 @@ class NativeNotifierPool:
                 else:
                     self.log.error(msg)
             elog.flush()
+        if hist is not None:
+            h_lat, s_lat, h_rtt, s_rtt, n = hist
+            self.metrics.latency.add_counts(array.array("Q", h_lat), s_lat, n)
+            self.metrics.rtt.add_counts(array.array("Q", h_rtt), s_rtt, n)
         if lat:
-            self.metrics.latency.observe_many(array.array("q", lat))
+            self.metrics.latency.add_samples(array.array("q", lat))
         for i in need_connect:
             self._schedule_connect(i, failed=(i == connect_failed))
         for i in want_write:

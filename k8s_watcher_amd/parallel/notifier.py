@@ -421,7 +421,9 @@ class NotifierPool:
     def _delivered(self, req: NotifyRequest) -> None:
         m = self.metrics
         m.c["notify_delivered"] += 1
-        m.latency.observe_ns(time.monotonic_ns() - req.read_ns)
+        now = time.monotonic_ns()
+        m.latency.observe_ns(now - req.read_ns)
+        m.rtt.observe_ns(now - req.sent_ns)
         if self.latest.get(req.uid) == req.seq:
             del self.latest[req.uid]
         if self.log_events:

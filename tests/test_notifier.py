@@ -3,6 +3,7 @@ timeouts, per-pod ordering, superseding, coalescing and backpressure."""
 
 import asyncio
 import random
+import time
 
 import pytest
 
@@ -255,3 +256,22 @@ def test_health_check(pool_cls):
         return ok, nok
 
     assert run(body()) == (True, False)
+
+
+def test_latency_and_rtt_histograms(pool_cls):
+    """Both pools fill the event->ack latency and request->ack RTT histograms
+    (the native core buckets them in C++; raw samples only with record_samples)."""
+    async def body():
+        sink, pool, m = await with_pool(pool_cls, sink_kwargs={"latency": 0.002})
+        for i in range(20):
+            pool.submit(f"u{i}", "ADDED", "default", f"p{i}", core(f"u{i}"), time.monotonic_ns(), TS)
+        pool.flush()
+        assert await pool.drain(5)
+        assert m.latency.n == 20 and m.rtt.n == 20
+        assert len(m.latency.samples) == 20
+        assert m.rtt.percentile_ns(50) >= 2e6 and m.latency.total_ns >= m.rtt.total_ns
+        text = m.prometheus_text()
+        assert 'k8s_watcher_notify_rtt_seconds_count 20' in text
+        assert 'k8s_watcher_notify_latency_seconds_count 20' in text
+        await close(sink, pool)
+    run(body())
