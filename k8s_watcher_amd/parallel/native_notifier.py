@@ -75,6 +75,9 @@ class NativeNotifierPool:
             sorted(RETRYABLE_STATUS), self.metrics.c)
         # histograms accumulate in C++; raw samples only when the Metrics keep them (benchmarks)
         self.core.set_histograms(_BUCKETS_NS, self.metrics.record_samples)
+        if settings.rate_limit_qps > 0:
+            self.core.set_rate_limit(settings.rate_limit_qps, settings.rate_limit_burst)
+        self._throttle_timer: Optional[asyncio.TimerHandle] = None
         if self.tls:  # TLS runs inside the core (OpenSSL on the same non-blocking sockets)
             self.core.enable_tls(self.host, settings.ca_file, settings.verify_tls)
         self.n = settings.pool.connections
@@ -165,6 +168,8 @@ class NativeNotifierPool:
     async def close(self) -> None:
         self.closing = True
         self._watchdog.cancel()
+        if self._throttle_timer is not None:
+            self._throttle_timer.cancel()
         for h in self.reconnect.values():
             h.cancel()
         for i in list(self.socks):
@@ -246,12 +251,18 @@ class NativeNotifierPool:
             self.writers.discard(i)
         self._after()
 
+    def _unthrottle(self) -> None:
+        self._throttle_timer = None
+        self.flush()
+
     def _requeue(self, seq: int) -> None:
         self.core.requeue(seq, self.closing)
         self._after()
 
     def _after(self, connect_failed: Optional[int] = None) -> None:
-        retries, logs, need_connect, want_write, lost, lat, spooled, hist = self.core.take()
+        retries, logs, need_connect, want_write, lost, lat, spooled, hist, throttle = self.core.take()
+        if throttle >= 0 and self._throttle_timer is None and not self.closing:
+            self._throttle_timer = self.loop.call_later(throttle, self._unthrottle)
         if spooled:
             for uid in self.spool.append(spooled):
                 self.core.spool_watch(uid, True)

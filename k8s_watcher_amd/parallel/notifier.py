@@ -183,7 +183,10 @@ class _Conn(asyncio.Protocol):
         now = time.monotonic_ns()
         head = self.pool.request_head
         unsent = self.pool.unsent
+        pool = self.pool
         while queue and len(inflight) < depth:
+            if pool.rl_qps and not pool._take_token(self):
+                break  # rate limited: the pool re-pumps this connection when a token is due
             req = queue.popleft()
             if unsent.get(req.uid) is req:
                 del unsent[req.uid]
@@ -253,6 +256,13 @@ class NotifierPool:
         self._dirty: List[_Conn] = []
         self._flush_scheduled = False
         self.retry_policy = settings.retry
+        # clusterapi.rate_limit: token bucket over all connections
+        self.rl_qps = settings.rate_limit_qps
+        self.rl_burst = settings.rate_limit_burst
+        self.rl_tokens = self.rl_burst
+        self.rl_last = time.monotonic()
+        self._throttled: List[_Conn] = []
+        self._throttle_timer: Optional[asyncio.TimerHandle] = None
         # spool (parallel/spool.py): uid -> seq of the newest live submit, for uids with spooled records
         self.spool = None
         self.spool_watch: Dict[str, int] = {}
@@ -327,6 +337,24 @@ class NotifierPool:
             self._dirty.append(conn)
         self._add_pending(1)
 
+    def _take_token(self, conn: "_Conn") -> bool:
+        now = time.monotonic()
+        self.rl_tokens = min(self.rl_burst, self.rl_tokens + (now - self.rl_last) * self.rl_qps)
+        self.rl_last = now
+        if self.rl_tokens >= 1.0:
+            self.rl_tokens -= 1.0
+            return True
+        self._throttled.append(conn)
+        if self._throttle_timer is None and not self.closing:
+            self._throttle_timer = self.loop.call_later((1.0 - self.rl_tokens) / self.rl_qps, self._unthrottle)
+        return False
+
+    def _unthrottle(self) -> None:
+        self._throttle_timer = None
+        conns, self._throttled = self._throttled, []
+        for c in dict.fromkeys(conns):
+            c.pump()
+
     def flush(self) -> None:
         dirty = self._dirty
         if not dirty:
@@ -384,6 +412,8 @@ class NotifierPool:
     async def close(self) -> None:
         self.closing = True
         self._watchdog.cancel()
+        if self._throttle_timer is not None:
+            self._throttle_timer.cancel()
         owed: List[NotifyRequest] = list(self.retrying.values())
         self.retrying.clear()
         for c in self.conns:

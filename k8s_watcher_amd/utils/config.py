@@ -239,6 +239,8 @@ class ClusterApiSettings:
     ca_file: Optional[str] = None
     health_check_on_start: bool = True
     spool: SpoolSettings = field(default_factory=SpoolSettings)
+    rate_limit_qps: float = 0.0  # clusterapi.rate_limit.qps; 0 = unlimited
+    rate_limit_burst: float = 100.0
 
 
 @dataclass
@@ -467,6 +469,9 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         ca_file=c.get("ca_file") or None,
         health_check_on_start=_as_bool(c.get("health_check_on_start", True), "clusterapi.health_check_on_start"),
         spool=_spool(c.get("spool") or {}),
+        rate_limit_qps=max(0.0, _as_float((c.get("rate_limit") or {}).get("qps", 0), "clusterapi.rate_limit.qps")),
+        rate_limit_burst=max(1.0, _as_float((c.get("rate_limit") or {}).get("burst", 100),
+                                            "clusterapi.rate_limit.burst")),
     )
 
     metrics = MetricsSettings(

@@ -275,3 +275,21 @@ def test_latency_and_rtt_histograms(pool_cls):
         assert 'k8s_watcher_notify_latency_seconds_count 20' in text
         await close(sink, pool)
     run(body())
+
+
+def test_rate_limit_paces_requests(pool_cls):
+    """clusterapi.rate_limit: a burst goes out at once, the rest at `qps`."""
+    async def body():
+        sink, pool, m = await with_pool(pool_cls, rate_limit_qps=200.0, rate_limit_burst=10.0, depth=4)
+        t0 = time.monotonic()
+        for i in range(50):
+            pool.submit(f"u{i}", "ADDED", "default", f"p{i}", core(f"u{i}"), 0, TS)
+        pool.flush()
+        await asyncio.sleep(0.05)
+        early = sink.state.count
+        assert 10 <= early <= 22  # the burst plus ~10 refilled tokens
+        assert await pool.drain(5)
+        took = time.monotonic() - t0
+        assert sink.state.count == 50 and 0.15 <= took <= 1.5  # 40 beyond the burst at 200/s ~ 0.2 s
+        await close(sink, pool)
+    run(body())
