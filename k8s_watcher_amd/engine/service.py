@@ -278,13 +278,26 @@ class WatcherService:
         them on restart; the previous (quiescent) checkpoint replays them
         instead. ``checkpoint=False`` (a leader that lost its lease) never
         writes — the new leader owns the file now.
+
+        With a spool, notifications still owed after the drain are written to
+        it first (closing the notifier), so the checkpoint can be written
+        anyway: a restart resumes exactly and replays the spool. A leader that
+        lost its lease drops what it still owes instead of spooling it — the
+        new leader relists, and an old record replayed in a later term could
+        overwrite newer state.
         """
         self.log.info("Stopping Pod watcher...")
         for r in self.reflectors:
             r.stop()
         drained = True
+        closed = False
         if self.notifier is not None:
+            if not checkpoint and self.spool is not None:
+                self.notifier.detach_spool()
             drained = await self.notifier.drain(drain_timeout)
+            if not drained and checkpoint and self.spool is not None:
+                await self.notifier.close()  # spools the rest
+                closed = drained = True
         if checkpoint and drained:
             await self._write_checkpoint()
         for t in self._tasks:
@@ -297,7 +310,7 @@ class WatcherService:
                 pass
         if self._metrics_server is not None:
             self._metrics_server.close()
-        if self.notifier is not None:
+        if self.notifier is not None and not closed:
             await self.notifier.close()  # with a spool, whatever is still owed is written to it
         if self.spool is not None:
             self.spool.close()

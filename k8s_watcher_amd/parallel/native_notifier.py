@@ -103,6 +103,11 @@ class NativeNotifierPool:
         for uid in spool.uid_counts:
             self.core.spool_watch(uid, True)
 
+    def detach_spool(self) -> None:
+        """Stop spooling: what fails or is left at close is dropped again."""
+        self.spool = None
+        self.core.spool_control(False)
+
     def replay(self, records) -> int:
         """Resubmit spooled records that are not stale; returns how many were submitted."""
         n = 0
@@ -263,7 +268,7 @@ class NativeNotifierPool:
         retries, logs, need_connect, want_write, lost, lat, spooled, hist, throttle = self.core.take()
         if throttle >= 0 and self._throttle_timer is None and not self.closing:
             self._throttle_timer = self.loop.call_later(throttle, self._unthrottle)
-        if spooled:
+        if spooled and self.spool is not None:
             for uid in self.spool.append(spooled):
                 self.core.spool_watch(uid, True)
         for i in lost:

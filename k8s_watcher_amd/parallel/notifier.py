@@ -277,6 +277,10 @@ class NotifierPool:
         for uid in spool.uid_counts:
             self.spool_watch.setdefault(uid, 0)
 
+    def detach_spool(self) -> None:
+        """Stop spooling: what fails or is left at close is dropped again."""
+        self.spool = None
+
     def replay(self, records) -> int:
         """Resubmit spooled records that are not stale; returns how many were submitted."""
         n = 0

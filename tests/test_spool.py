@@ -209,3 +209,47 @@ def test_service_outage_recovery_with_spool(tmp_path):
         await sink.stop()
         await srv.stop()
     run(body())
+
+
+def test_shutdown_with_owed_notifications_spools_then_checkpoints(tmp_path):
+    """Checkpoint + spool: a shutdown during an outage spools what is owed and
+    still writes the checkpoint; the restart resumes from it and replays the
+    spool — every pod reaches clusterapi exactly once, nothing is relisted as new."""
+    from test_e2e_slice import start_stack
+    from k8s_watcher_amd.testing.podgen import PodFactory
+
+    async def body():
+        ov = {"clusterapi": {"retry": {"max_attempts": 50, "delay_seconds": 0.05},
+                             "spool": {"path": str(tmp_path / "spool"), "replay_interval_seconds": 0.05}},
+              "watcher": {"checkpoint": {"path": str(tmp_path / "ck.json"), "interval_seconds": 60}}}
+        srv, sink, svc = await start_stack("staging", overrides=ov)
+        await svc.start()
+        f = PodFactory(seed=41, namespaces=["default"])
+        sink.state.down = True
+        pods = [f.running(f.new_pod()) for _ in range(5)]
+        for p in pods:
+            srv.create(p)
+        for _ in range(200):
+            if svc.metrics.c["events_received"] >= 5:
+                break
+            await asyncio.sleep(0.02)
+        svc.stop()
+        await svc.shutdown(drain_timeout=0.2)
+        assert svc.metrics.c["notify_spooled"] == 5 and svc.metrics.c["checkpoints_written"] == 1
+        sink.state.down = False
+        # restart on the same checkpoint and spool
+        from k8s_watcher_amd.engine.service import WatcherService
+        from k8s_watcher_amd.kube.kubeconfig import KubeEndpoint
+        from k8s_watcher_amd.metrics import Metrics
+        svc2 = WatcherService(svc.settings, endpoint=KubeEndpoint(server=srv.url), metrics=Metrics())
+        await svc2.start()
+        await sink.state.wait_for(5, timeout=10)
+        await asyncio.sleep(0.3)
+        got = sorted(p["uid"] for p in sink.state.payloads())
+        assert got == sorted(p["metadata"]["uid"] for p in pods)  # once each: replayed, not relisted
+        assert svc2.metrics.c["spool_replayed"] == 5
+        svc2.stop()
+        await svc2.shutdown()
+        await sink.stop()
+        await srv.stop()
+    run(body())
