@@ -61,6 +61,7 @@ def parse_args(argv=None):
     ap.add_argument("--pipeline-depth", type=int, default=None)
     ap.add_argument("--decode-threads", default=None, help="watcher.decode_threads (int or auto)")
     ap.add_argument("--decode-affinity", default=None, choices=["auto", "none", "l3"])
+    ap.add_argument("--watch-read-bytes", type=int, default=None, help="watcher.watch_read_bytes")
     ap.add_argument("--no-placement", dest="placement", action="store_false",
                     help="no per-rank L3 domain assignment (each watcher still pins per watcher.decode_affinity)")
     ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
@@ -200,6 +201,7 @@ async def rank_main(args, d: Dist) -> dict:
                            "enabled": not os.environ.get("BENCH_NO_NOTIFY")},
             "watcher": {"engine": args.engine, "retry": {"max_attempts": 0, "delay_seconds": 0.05},
                         **({"decode_threads": args.decode_threads} if args.decode_threads is not None else {}),
+                        **({"watch_read_bytes": args.watch_read_bytes} if args.watch_read_bytes else {}),
                         # placement already pinned this thread (the decode workers inherit it)
                         **({"decode_affinity": args.decode_affinity or ("none" if watcher_cpus else "auto")})},
         }
@@ -412,6 +414,9 @@ def main(argv=None) -> int:
         "notified_per_s": round(notified / elapsed, 1),
         "notify_failed": res["failed"],
         "cpu_util_rank0": res["cpu_util"],
+        # the watcher's own efficiency (the rate is bound by the replay fixture's core when it hits 1.0)
+        "events_per_watcher_cpu_second": (round(res["events"] / (res["cpu_util"]["watcher"] * res["elapsed"]), 1)
+                                          if res["cpu_util"].get("watcher") else None),
         "placement_rank0": res["placement"],
         "saturated_p50_latency_ms": round(res["sat_p50_ns"] / 1e6, 3) if res["sat_p50_ns"] else None,
         "reference_equiv": ({"events_per_s": round(ref_rate, 1), "events": ref["events"],

@@ -526,8 +526,8 @@ class HttpClient:
                      query: Optional[Dict[str, object]] = None,
                      headers: Optional[Dict[str, str]] = None,
                      timeout: Optional[float] = None, raw_chunked: bool = False,
-                     on_mode: Optional[Callable[[bool], None]] = None
-                     ) -> Tuple[StreamResponse, Optional[bytes]]:
+                     on_mode: Optional[Callable[[bool], None]] = None,
+                     read_size: int = 0) -> Tuple[StreamResponse, Optional[bytes]]:
         """Start a request whose body is streamed to ``sink(data, read_ns)``.
 
         With ``raw_chunked`` a 2xx chunked body is passed through *with* its
@@ -536,11 +536,17 @@ class HttpClient:
 
         Returns ``(stream, error_body)``: for a non-2xx status the whole body
         is read and returned as ``error_body`` and the connection is closed.
+
+        ``read_size`` raises the bytes taken per socket read on a plain TCP
+        stream (asyncio's default is 256 KiB): a busy watch then costs fewer
+        event-loop iterations and fewer decoder calls per event.
         """
         tmo = self.timeout if timeout is None else timeout
         target = self.url_target(path, query)
         raw = build_request(method, target, self.host_header, self._merged_headers(headers), None)
         proto = await self._connect(tmo)
+        if read_size > 0 and self.ssl_context is None and hasattr(proto.transport, "max_size"):
+            proto.transport.max_size = read_size  # selector transport: recv() size per readiness event
         loop = asyncio.get_running_loop()
         proto.busy = True
         head_fut = loop.create_future()

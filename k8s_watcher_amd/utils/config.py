@@ -284,6 +284,7 @@ class WatcherSettings:
     initial_list: str = "notify"  # notify | skip
     initial_sync: str = "list"  # list | watch_list (sendInitialEvents, LIST fallback)
     watch_list_idle_seconds: float = 5.0
+    watch_read_bytes: int = 4 << 20  # bytes per socket read on a plain-TCP watch (asyncio default 256 KiB)
     retry: RetryPolicy = field(default_factory=lambda: RetryPolicy(3, 5.0))
     watch_timeout_seconds: int = 300
     list_page_size: int = 500
@@ -428,6 +429,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         initial_list=_choice(w.get("initial_list", "notify"), "watcher.initial_list", ("notify", "skip")),
         initial_sync=_choice(w.get("initial_sync", "list"), "watcher.initial_sync", ("list", "watch_list")),
         watch_list_idle_seconds=_as_float(w.get("watch_list_idle_seconds", 5), "watcher.watch_list_idle_seconds"),
+        watch_read_bytes=max(0, _as_int(w.get("watch_read_bytes", 4 << 20), "watcher.watch_read_bytes")),
         retry=_retry(w.get("retry"), "watcher.retry", RetryPolicy(3, 5.0), min_attempts=0),
         watch_timeout_seconds=_as_int(w.get("watch_timeout_seconds", 300), "watcher.watch_timeout_seconds"),
         list_page_size=max(1, _as_int(w.get("list_page_size", 500), "watcher.list_page_size")),
