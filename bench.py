@@ -16,14 +16,12 @@ namespace shards, weak scaling):
   real-shaped Pod JSON per event, one HTTP chunk per event);
 * a stub clusterapi child (``testing/stub_sink.py``) acks every POST;
 * this process runs the real :class:`WatcherService` (production profile:
-  critical-events filter, namespace filter, notifier pool); every event is
-  decoded and filtered and — if it survived the filters — POSTed and
-  acknowledged (2xx) by the sink.
+  critical-events filter, namespace filter, notifier pool) and a step ends when
+  every event of the step has been decoded, filtered and — if it survived the
+  filters — POSTed and acknowledged (2xx) by the sink.
 
-``W`` warmup steps run untimed (each waits for its last ack), then exactly
-``K`` steps are timed between barriers, streamed back to back (step k+1
-starts once step k is decoded); the clock stops when every notification of
-the K steps is acknowledged. The slowest rank's time is used. Latency (socket read of the watch
+``W`` warmup steps run untimed, then exactly ``K`` steps are timed between
+barriers; the slowest rank's time is used. Latency (socket read of the watch
 chunk → 2xx from clusterapi) is measured afterwards at the config's nominal
 rate (``--latency-rate``, default 100 ev/s as in config #4).
 
@@ -234,16 +232,14 @@ async def rank_main(args, d: Dist) -> dict:
 
         debug = bool(os.environ.get("BENCH_DEBUG"))
 
-        async def run_step(k: int, pace: str = "", acked: bool = True) -> None:
-            """Stream step ``k``; return once all its events are decoded (and, with
-            ``acked``, every resulting notification has its 2xx)."""
+        async def run_step(k: int, pace: str = "") -> None:
             base = c["events_received"]
             t_start = time.perf_counter()
             n = await cmd(f"PACE {k} {pace}" if pace else f"STEP {k}")
             t_sent = time.perf_counter()
             t_ingest = None
             deadline = time.monotonic() + args.step_timeout
-            while c["events_received"] < base + n or (acked and svc.notifier.outstanding() > 0):
+            while c["events_received"] < base + n or svc.notifier.outstanding() > 0:
                 if t_ingest is None and c["events_received"] >= base + n:
                     t_ingest = time.perf_counter()
                 if time.monotonic() > deadline:
@@ -262,17 +258,8 @@ async def rank_main(args, d: Dist) -> dict:
         n0, s0 = c["events_received"], c["notify_delivered"]
         cpu0 = cpu_snapshot(replay.pid, sink.pid)
         t0 = time.perf_counter()
-        # Timed steps stream back to back: step k+1 starts once step k is decoded,
-        # so the notification tail of one step overlaps the next (a sustained
-        # stream, as from a real API server). The clock stops only when every
-        # notification of all K steps has been acknowledged.
         for k in range(args.warmup, args.warmup + args.steps):
-            await run_step(k, acked=False)
-        deadline = time.monotonic() + args.step_timeout
-        while svc.notifier.outstanding() > 0:
-            if time.monotonic() > deadline:
-                raise TimeoutError(f"{svc.notifier.outstanding()} notifications outstanding after the last step")
-            await asyncio.sleep(0.0005)
+            await run_step(k)
         elapsed = time.perf_counter() - t0
         cpu1 = cpu_snapshot(replay.pid, sink.pid)
         d.barrier()
