@@ -287,7 +287,11 @@ async def rank_main(args, d: Dist) -> dict:
         return {"elapsed": elapsed, "events": events, "notified": notified, "events_per_step": events_per_step,
                 "p50_ns": p50, "p99_ns": p99, "lat_samples": lat_n, "sat_p50_ns": sat_p50,
                 "failed": failed, "ref": ref,
-                "cpu_util": {k: round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0},
+                "cpu_util": {k: round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0
+                             if not k.startswith("thread_") or k == "thread_loop"},
+                "cpu_threads": sorted((round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0
+                                       if k.startswith("thread_") and k != "thread_loop" and k in cpu1),
+                                      reverse=True)[:8],
                 "decode_threads": decode_threads,
                 "placement": {"watcher": cpu_ranges(watcher_cpus)}}
     finally:
@@ -329,7 +333,11 @@ def cpu_snapshot(replay_pid: int, sink_pid: int) -> dict:
         return tot
 
     t = os.times()
-    return {"watcher": t.user + t.system, "replay": tree(replay_pid), "sink": tree(sink_pid)}
+    out = {"watcher": t.user + t.system, "replay": tree(replay_pid), "sink": tree(sink_pid)}
+    main = threading.get_native_id()
+    for th in psutil.Process().threads():  # per thread: the event loop vs the decode workers
+        out["thread_loop" if th.id == main else f"thread_{th.id}"] = th.user_time + th.system_time
+    return out
 
 
 async def run_reference(args, api_port: int, sink_url: str, cmd, step: int, ca_file=None) -> dict:
@@ -414,6 +422,7 @@ def main(argv=None) -> int:
         "notified_per_s": round(notified / elapsed, 1),
         "notify_failed": res["failed"],
         "cpu_util_rank0": res["cpu_util"],
+        "cpu_other_threads_rank0": res["cpu_threads"],
         # the watcher's own efficiency (the rate is bound by the replay fixture's core when it hits 1.0)
         "events_per_watcher_cpu_second": (round(res["events"] / (res["cpu_util"]["watcher"] * res["elapsed"]), 1)
                                           if res["cpu_util"].get("watcher") else None),
