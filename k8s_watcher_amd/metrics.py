@@ -54,61 +54,92 @@ _BUCKETS_NS = [int(10 ** (3 + i / 4)) for i in range(0, 33)]
 
 
 class LatencyHistogram:
+    """Log-bucketed histogram. Besides direct observations it can pull from
+    *sources* — callables returning cumulative ``(counts, total_ns, n)`` kept
+    elsewhere (the native notifier core buckets in C++) — merged lazily when the
+    histogram is read, so the hot path does no per-notification Python work."""
+
     def __init__(self, record_samples: bool = False) -> None:
-        self.counts = [0] * (len(_BUCKETS_NS) + 1)
-        self.total_ns = 0
-        self.n = 0
+        self._counts = [0] * (len(_BUCKETS_NS) + 1)
+        self._total_ns = 0
+        self._n = 0
         self.samples: Optional[array.array] = array.array("q") if record_samples else None
+        self._sources: List[list] = []  # [fn, last counts, last total, last n]
+
+    def add_source(self, fn: Callable[[], tuple]) -> None:
+        counts, total, n = fn()
+        self._sources.append([fn, list(counts), total, n])  # start from the current totals
+
+    def sync(self) -> None:
+        for src in self._sources:
+            counts, total, n = src[0]()
+            if n == src[3]:
+                continue
+            c, last = self._counts, src[1]
+            for i, v in enumerate(counts):
+                if v != last[i]:
+                    c[i] += v - last[i]
+            self._total_ns += total - src[2]
+            self._n += n - src[3]
+            src[1], src[2], src[3] = list(counts), total, n
+
+    @property
+    def counts(self) -> List[int]:
+        self.sync()
+        return self._counts
+
+    @property
+    def total_ns(self) -> int:
+        self.sync()
+        return self._total_ns
+
+    @property
+    def n(self) -> int:
+        self.sync()
+        return self._n
 
     def observe_ns(self, ns: int) -> None:
-        self.counts[bisect.bisect_left(_BUCKETS_NS, ns)] += 1
-        self.total_ns += ns
-        self.n += 1
+        self._counts[bisect.bisect_left(_BUCKETS_NS, ns)] += 1
+        self._total_ns += ns
+        self._n += 1
         if self.samples is not None:
             self.samples.append(ns)
 
     def observe_many(self, values: "array.array") -> None:
         """Bulk observe (int64 nanoseconds), e.g. latencies reported by the native notifier."""
-        counts = self.counts
+        counts = self._counts
         bl = bisect.bisect_left
         for ns in values:
             counts[bl(_BUCKETS_NS, ns)] += 1
-        self.total_ns += sum(values)
-        self.n += len(values)
+        self._total_ns += sum(values)
+        self._n += len(values)
         if self.samples is not None:
             self.samples.extend(values)
-
-    def add_counts(self, counts: "array.array", total_ns: int, n: int) -> None:
-        """Merge bucket counts computed elsewhere (the native notifier core)."""
-        c = self.counts
-        for i, v in enumerate(counts):
-            if v:
-                c[i] += v
-        self.total_ns += total_ns
-        self.n += n
 
     def add_samples(self, values: "array.array") -> None:
         if self.samples is not None:
             self.samples.extend(values)
 
     def reset(self) -> None:
-        self.counts = [0] * (len(_BUCKETS_NS) + 1)
-        self.total_ns = 0
-        self.n = 0
+        self.sync()  # sources restart from their current totals
+        self._counts = [0] * (len(_BUCKETS_NS) + 1)
+        self._total_ns = 0
+        self._n = 0
         if self.samples is not None:
             self.samples = array.array("q")
 
     def percentile_ns(self, q: float) -> Optional[float]:
         """Exact when samples are recorded, otherwise bucket upper bound."""
-        if self.n == 0:
+        n = self.n  # syncs
+        if n == 0:
             return None
         if self.samples is not None and len(self.samples):
             s = sorted(self.samples)
             k = max(0, min(len(s) - 1, int(math.ceil(q / 100.0 * len(s))) - 1))
             return float(s[k])
-        target = q / 100.0 * self.n
+        target = q / 100.0 * n
         acc = 0
-        for i, c in enumerate(self.counts):
+        for i, c in enumerate(self._counts):
             acc += c
             if acc >= target:
                 return float(_BUCKETS_NS[i] if i < len(_BUCKETS_NS) else _BUCKETS_NS[-1])

@@ -75,6 +75,8 @@ class NativeNotifierPool:
             sorted(RETRYABLE_STATUS), self.metrics.c)
         # histograms accumulate in C++; raw samples only when the Metrics keep them (benchmarks)
         self.core.set_histograms(_BUCKETS_NS, self.metrics.record_samples)
+        self.metrics.latency.add_source(lambda: self._hist(0))
+        self.metrics.rtt.add_source(lambda: self._hist(1))
         if settings.rate_limit_qps > 0:
             self.core.set_rate_limit(settings.rate_limit_qps, settings.rate_limit_burst)
         self._throttle_timer: Optional[asyncio.TimerHandle] = None
@@ -256,6 +258,10 @@ class NativeNotifierPool:
             self.writers.discard(i)
         self._after()
 
+    def _hist(self, which: int):
+        h_lat, s_lat, h_rtt, s_rtt, n = self.core.histograms()
+        return (array.array("Q", h_rtt if which else h_lat), s_rtt if which else s_lat, n)
+
     def _unthrottle(self) -> None:
         self._throttle_timer = None
         self.flush()
@@ -265,7 +271,7 @@ class NativeNotifierPool:
         self._after()
 
     def _after(self, connect_failed: Optional[int] = None) -> None:
-        retries, logs, need_connect, want_write, lost, lat, spooled, hist, throttle = self.core.take()
+        retries, logs, need_connect, want_write, lost, lat, spooled, throttle = self.core.take()
         if throttle >= 0 and self._throttle_timer is None and not self.closing:
             self._throttle_timer = self.loop.call_later(throttle, self._unthrottle)
         if spooled and self.spool is not None:
@@ -285,10 +291,6 @@ class NativeNotifierPool:
                 else:
                     self.log.error(msg)
             elog.flush()
-        if hist is not None:
-            h_lat, s_lat, h_rtt, s_rtt, n = hist
-            self.metrics.latency.add_counts(array.array("Q", h_lat), s_lat, n)
-            self.metrics.rtt.add_counts(array.array("Q", h_rtt), s_rtt, n)
         if lat:
             self.metrics.latency.add_samples(array.array("q", lat))
         for i in need_connect:
