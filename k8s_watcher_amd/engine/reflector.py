@@ -285,7 +285,8 @@ class Reflector:
             sink, namespace=self.namespace, resource_version=self.rv,
             timeout_seconds=w.watch_timeout_seconds or None, allow_bookmarks=True,
             label_selector=w.label_selector, field_selector=w.field_selector,
-            raw_chunked=True, on_mode=on_mode, read_size=w.watch_read_bytes)
+            raw_chunked=True, on_mode=on_mode, read_size=w.watch_read_bytes,
+            zero_copy=native is not None)  # the fused pipeline copies what it keeps (partial lines)
         self.watch_count += 1
         self.connected.set()
         if self._stop.is_set():

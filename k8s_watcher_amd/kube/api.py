@@ -94,7 +94,8 @@ class KubeApi:
                          field_selector: Optional[str] = None,
                          connect_timeout: Optional[float] = None, raw_chunked: bool = False,
                          on_mode: Optional[Callable[[bool], None]] = None,
-                         send_initial_events: bool = False, read_size: int = 0) -> StreamResponse:
+                         send_initial_events: bool = False, read_size: int = 0,
+                         zero_copy: bool = False) -> StreamResponse:
         """Open ``?watch=true``; body bytes go to ``sink(data, read_ns)``.
 
         With ``raw_chunked`` the HTTP chunk framing is left in place for the
@@ -119,7 +120,7 @@ class KubeApi:
             q["fieldSelector"] = field_selector
         stream, err = await self.http.stream("GET", pods_path(namespace), sink, query=q,
                                              timeout=connect_timeout, raw_chunked=raw_chunked,
-                                             on_mode=on_mode, read_size=read_size)
+                                             on_mode=on_mode, read_size=read_size, zero_copy=zero_copy)
         if err is not None:
             raise ApiError(stream.status, stream.reason, err)
         return stream

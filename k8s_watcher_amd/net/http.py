@@ -299,11 +299,23 @@ def response_scanner(native: bool = True):
     return PyResponseScanner()
 
 
-class _ClientProtocol(asyncio.Protocol):
-    """One TCP/TLS connection; at most one outstanding request (no pipelining here)."""
+class _ClientProtocol(asyncio.BufferedProtocol):
+    """One TCP/TLS connection; at most one outstanding request (no pipelining here).
+
+    A buffered protocol: the transport ``recv_into``s a buffer owned here
+    (``read_size`` bytes, reused). With ``zero_copy`` set (a stream whose sink
+    does not keep the data past the call — the native watch pipeline), body
+    bytes in RAW mode reach the sink as a ``memoryview`` of that buffer: no
+    per-read allocation or copy on the event-loop thread. Everything else gets
+    ``bytes`` as before.
+    """
+
+    read_size = 256 * 1024
 
     def __init__(self, loop: asyncio.AbstractEventLoop) -> None:
         self.loop = loop
+        self._rbuf: Optional[bytearray] = None
+        self.zero_copy = False
         self.transport: Optional[asyncio.Transport] = None
         self.parser = ResponseParser()
         self.waiter: Optional[asyncio.Future] = None
@@ -323,6 +335,27 @@ class _ClientProtocol(asyncio.Protocol):
     # asyncio callbacks
     def connection_made(self, transport) -> None:  # type: ignore[override]
         self.transport = transport
+
+    def get_buffer(self, sizehint: int) -> bytearray:  # type: ignore[override]
+        b = self._rbuf
+        if b is None or len(b) != self.read_size:
+            b = self._rbuf = bytearray(self.read_size)  # a fresh one: never resize an exported buffer
+        return b
+
+    def buffer_updated(self, nbytes: int) -> None:  # type: ignore[override]
+        p = self.parser
+        if self.zero_copy and p.state == ResponseParser.RAW and not p.buf and p.on_body is not None:
+            now = time.monotonic_ns()
+            self.read_stamp = now
+            self.last_activity = now * 1e-9
+            try:
+                p.on_body(memoryview(self._rbuf)[:nbytes])
+            except Exception as exc:  # noqa: BLE001
+                self._fail(exc)
+                if self.transport is not None:
+                    self.transport.close()
+            return
+        self.data_received(bytes(memoryview(self._rbuf)[:nbytes]))
 
     def data_received(self, data: bytes) -> None:  # type: ignore[override]
         now = time.monotonic_ns()
@@ -527,7 +560,7 @@ class HttpClient:
                      headers: Optional[Dict[str, str]] = None,
                      timeout: Optional[float] = None, raw_chunked: bool = False,
                      on_mode: Optional[Callable[[bool], None]] = None,
-                     read_size: int = 0) -> Tuple[StreamResponse, Optional[bytes]]:
+                     read_size: int = 0, zero_copy: bool = False) -> Tuple[StreamResponse, Optional[bytes]]:
         """Start a request whose body is streamed to ``sink(data, read_ns)``.
 
         With ``raw_chunked`` a 2xx chunked body is passed through *with* its
@@ -537,16 +570,21 @@ class HttpClient:
         Returns ``(stream, error_body)``: for a non-2xx status the whole body
         is read and returned as ``error_body`` and the connection is closed.
 
-        ``read_size`` raises the bytes taken per socket read on a plain TCP
-        stream (asyncio's default is 256 KiB): a busy watch then costs fewer
-        event-loop iterations and fewer decoder calls per event.
+        ``read_size`` raises the bytes taken per socket read (default 256
+        KiB): a busy watch then costs fewer event-loop iterations and fewer
+        decoder calls per event. ``zero_copy`` hands RAW body bytes to
+        ``sink`` as a ``memoryview`` of the protocol's reused read buffer; the
+        sink must not keep it past the call.
         """
         tmo = self.timeout if timeout is None else timeout
         target = self.url_target(path, query)
         raw = build_request(method, target, self.host_header, self._merged_headers(headers), None)
         proto = await self._connect(tmo)
-        if read_size > 0 and self.ssl_context is None and hasattr(proto.transport, "max_size"):
-            proto.transport.max_size = read_size  # selector transport: recv() size per readiness event
+        if read_size > 0:
+            proto.read_size = read_size  # plain TCP: recv_into this many bytes per readiness event
+            if hasattr(proto.transport, "max_size"):
+                proto.transport.max_size = read_size
+        proto.zero_copy = zero_copy
         loop = asyncio.get_running_loop()
         proto.busy = True
         head_fut = loop.create_future()
