@@ -24,6 +24,8 @@
 #include <openssl/x509v3.h>
 
 #include <linux/futex.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <sys/syscall.h>
 #include <sys/types.h>
@@ -38,6 +40,7 @@
 #include <ctime>
 #include <deque>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>

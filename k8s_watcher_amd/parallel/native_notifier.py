@@ -25,6 +25,7 @@ from __future__ import annotations
 import array
 import asyncio
 import logging
+import os
 import socket
 import time
 from typing import Callable, Dict, Optional
@@ -95,6 +96,13 @@ class NativeNotifierPool:
         self.on_saturation = on_saturation
         self.closing = False
         self.spool = None
+        # clusterapi.pool.io_thread: the core serves the sockets on its own
+        # thread (epoll) and signals this eventfd when Python has work to do
+        self.threaded = settings.pool.io_thread
+        self._py_fd = -1
+        if self.threaded:
+            self._py_fd = self.core.start_io()
+            self.loop.add_reader(self._py_fd, self._on_io_signal)
         self._watchdog = self.loop.create_task(self._watchdog_loop())
 
     # ------------------------------------------------------------------ spool (parallel/spool.py)
@@ -168,8 +176,10 @@ class NativeNotifierPool:
         deadline = None if timeout is None else self.loop.time() + timeout
         while self.core.pending() > 0:
             if deadline is not None and self.loop.time() > deadline:
+                self._after()
                 return False
             await asyncio.sleep(0.001)
+        self._after()  # counters, logs and samples of the last responses (I/O thread mode)
         return True
 
     async def close(self) -> None:
@@ -180,10 +190,14 @@ class NativeNotifierPool:
         for h in self.reconnect.values():
             h.cancel()
         for i in list(self.socks):
+            self.core.detach(i, "closing")  # deregisters the fd before the socket is closed
             self._drop_socket(i)
-            self.core.detach(i, "closing")
         self.core.give_up_all()
         self._after()
+        if self.threaded:
+            self.loop.remove_reader(self._py_fd)
+            self.core.stop_io()
+            self.threaded = False
         await asyncio.sleep(0)
 
     # ------------------------------------------------------------------ sockets
@@ -219,7 +233,8 @@ class NativeNotifierPool:
         self.socks[i] = sock
         self.backoff[i].reset()
         self.core.attach(i, sock.fileno())
-        self.loop.add_reader(sock.fileno(), self._readable, i)
+        if not self.threaded:
+            self.loop.add_reader(sock.fileno(), self._readable, i)
         self.core.flush()
         self._after()
 
@@ -239,13 +254,21 @@ class NativeNotifierPool:
         if sock is None:
             return
         fd = sock.fileno()
-        self.loop.remove_reader(fd)
+        if not self.threaded:
+            self.loop.remove_reader(fd)
         if i in self.writers:
             self.loop.remove_writer(fd)
             self.writers.discard(i)
         sock.close()
 
     # ------------------------------------------------------------------ loop callbacks
+    def _on_io_signal(self) -> None:
+        try:
+            os.read(self._py_fd, 8)
+        except BlockingIOError:
+            pass
+        self._after()
+
     def _readable(self, i: int) -> None:
         self.core.on_readable(i)
         self._after()
@@ -303,6 +326,8 @@ class NativeNotifierPool:
         pending = self.core.pending()
         if not self.saturated and pending >= self.high_water:
             self.saturated = True
+            if self.threaded:  # the I/O thread wakes us when the queue has drained enough
+                self.core.signal_below(self.low_water)
             if self.on_saturation:
                 self.on_saturation(True)
         elif self.saturated and pending <= self.low_water:
@@ -317,6 +342,6 @@ class NativeNotifierPool:
             await asyncio.sleep(period)
             for i in self.core.check_timeouts(timeout_ns):
                 self.log.error(f"Timeout error: Request to {self.endpoint_url} timed out")
-                self._drop_socket(i)
                 self.core.detach(i, f"Timeout error: Request to {self.endpoint_url} timed out")
+                self._drop_socket(i)
             self._after()

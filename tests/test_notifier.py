@@ -31,10 +31,18 @@ def core(uid, phase="Running", name=None):
     return build_core(pod, "production")
 
 
-@pytest.fixture(params=["python", "native"])
+def _inline_native(s, metrics=None, **kw):
+    """The native core driven from the event loop (``clusterapi.pool.io_thread: false``)."""
+    import dataclasses
+    return NativeNotifierPool(dataclasses.replace(s, pool=dataclasses.replace(s.pool, io_thread=False)),
+                              metrics, **kw)
+
+
+@pytest.fixture(params=["python", "native", "native-inline"])
 def pool_cls(request):
-    """Every test runs against the asyncio pool and the native-core pool."""
-    return NotifierPool if request.param == "python" else NativeNotifierPool
+    """Every test runs against the asyncio pool and the native-core pool, the
+    latter with its own I/O thread (default) and driven from the event loop."""
+    return {"python": NotifierPool, "native": NativeNotifierPool, "native-inline": _inline_native}[request.param]
 
 
 async def with_pool(cls, sink_kwargs=None, **kw):
