@@ -65,8 +65,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-placement", dest="placement", action="store_false",
                     help="no per-rank L3 domain assignment (each watcher still pins per watcher.decode_affinity)")
     ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
-    ap.add_argument("--no-io-thread", dest="io_thread", action="store_false",
-                    help="drive the C++ notifier core from the event loop (clusterapi.pool.io_thread: false)")
+    ap.add_argument("--io-thread", action="store_true",
+                    help="serve the C++ notifier core's sockets on its own thread (clusterapi.pool.io_thread)")
     ap.add_argument("--tls", action="store_true",
                     help="https clusterapi (as production.yaml): the stub sink serves TLS with a throw-away CA")
     ap.add_argument("--sink-workers", type=int, default=4)
@@ -214,8 +214,8 @@ async def rank_main(args, d: Dist) -> dict:
             pool["pipeline_depth"] = args.pipeline_depth
         if args.python_pool:
             pool["native"] = False
-        if not args.io_thread:
-            pool["io_thread"] = False
+        if args.io_thread:
+            pool["io_thread"] = True
         if pool:
             overrides["clusterapi"]["pool"] = pool
         settings = load_settings(args.profile, overrides=overrides)

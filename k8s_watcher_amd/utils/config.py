@@ -211,7 +211,7 @@ class NotifierPoolSettings:
     queue_size: int = 65536
     coalesce: bool = False
     native: bool = True  # C++ notifier core (watcher.engine: native)
-    io_thread: bool = True  # native core serves its sockets on a dedicated thread
+    io_thread: bool = False  # native core serves its sockets on a dedicated thread (profiles/notifier_io_thread_gpu_box.md)
 
 
 @dataclass
@@ -467,7 +467,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
             queue_size=max(1, _as_int(pool.get("queue_size", 65536), "clusterapi.pool.queue_size")),
             coalesce=_as_bool(pool.get("coalesce", False), "clusterapi.pool.coalesce"),
             native=_as_bool(pool.get("native", True), "clusterapi.pool.native"),
-            io_thread=_as_bool(pool.get("io_thread", True), "clusterapi.pool.io_thread"),
+            io_thread=_as_bool(pool.get("io_thread", False), "clusterapi.pool.io_thread"),
         ),
         verify_tls=_as_bool(c.get("verify_tls", True), "clusterapi.verify_tls"),
         ca_file=c.get("ca_file") or None,

@@ -31,18 +31,18 @@ def core(uid, phase="Running", name=None):
     return build_core(pod, "production")
 
 
-def _inline_native(s, metrics=None, **kw):
-    """The native core driven from the event loop (``clusterapi.pool.io_thread: false``)."""
+def _threaded_native(s, metrics=None, **kw):
+    """The native core serving its sockets on its own thread (``clusterapi.pool.io_thread``)."""
     import dataclasses
-    return NativeNotifierPool(dataclasses.replace(s, pool=dataclasses.replace(s.pool, io_thread=False)),
+    return NativeNotifierPool(dataclasses.replace(s, pool=dataclasses.replace(s.pool, io_thread=True)),
                               metrics, **kw)
 
 
-@pytest.fixture(params=["python", "native", "native-inline"])
+@pytest.fixture(params=["python", "native", "native-io-thread"])
 def pool_cls(request):
     """Every test runs against the asyncio pool and the native-core pool, the
-    latter with its own I/O thread (default) and driven from the event loop."""
-    return {"python": NotifierPool, "native": NativeNotifierPool, "native-inline": _inline_native}[request.param]
+    latter driven from the event loop (default) and on its own I/O thread."""
+    return {"python": NotifierPool, "native": NativeNotifierPool, "native-io-thread": _threaded_native}[request.param]
 
 
 async def with_pool(cls, sink_kwargs=None, **kw):
