@@ -21,7 +21,7 @@ import time
 from k8s_watcher_amd.ops.native import load
 from k8s_watcher_amd.testing.replay_server import Template
 
-READ_SIZE = 256 * 1024  # asyncio's selector transports read at most this per recv
+READ_SIZE = 4 << 20  # watcher.watch_read_bytes default (bytes per socket read)
 
 
 def unframe(data: bytes) -> bytes:
@@ -34,8 +34,9 @@ def unframe(data: bytes) -> bytes:
     return bytes(out)
 
 
-def pipeline_rate(mod, data: bytes, n: int, threads: int, critical: bool, reps: int) -> float:
-    chunks = [data[j:j + READ_SIZE] for j in range(0, len(data), READ_SIZE)]
+def pipeline_rate(mod, data: bytes, n: int, threads: int, critical: bool, reps: int,
+                  read_size: int = READ_SIZE) -> float:
+    chunks = [data[j:j + read_size] for j in range(0, len(data), read_size)]
     best = float("inf")
     for _ in range(reps):
         pl = mod.Pipeline("production", mod.PodCache(), {}, None, critical, False, 1, 0, True, True, None,
@@ -57,6 +58,7 @@ def main(argv=None) -> int:
     ap.add_argument("--threads", default="0,1,2,3,5")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--read-size", type=int, default=READ_SIZE, help="bytes per simulated socket read")
     args = ap.parse_args(argv)
     mod = load()
     t = Template("churn", args.pods, 0)
@@ -75,7 +77,7 @@ def main(argv=None) -> int:
     res["simd"] = mod.cpu_features()
     for th in [int(x) for x in args.threads.split(",")]:
         for critical, profile in ((True, "production (critical filter)"), (False, "all events notified")):
-            rate = pipeline_rate(mod, data, n, th, critical, args.reps)
+            rate = pipeline_rate(mod, data, n, th, critical, args.reps, args.read_size)
             res["pipeline"].append({"decode_threads": th, "profile": profile, "events_per_s": round(rate)})
     print(f"# native pipeline ceiling, {n} events x {res['bytes_per_event']} B, SIMD {res['simd']}\n")
     print("| SIMD | skip | light extract | full extract | + payload core |  (ns/event, one thread)")
