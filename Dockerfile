@@ -1,12 +1,13 @@
 # k8s-watcher-amd — container image (SURVEY §2.2: the reference claims
 # "Dockerized" but ships no Dockerfile).
 FROM python:3.10-slim AS build
-RUN apt-get update && apt-get install -y --no-install-recommends g++ && rm -rf /var/lib/apt/lists/*
+RUN apt-get update && apt-get install -y --no-install-recommends g++ libssl-dev && rm -rf /var/lib/apt/lists/*
 WORKDIR /app
 COPY k8s_watcher_amd/ k8s_watcher_amd/
 RUN pip install --no-cache-dir pyyaml && python -m k8s_watcher_amd.ops.native
 
 FROM python:3.10-slim
+# runtime: libssl3 (the notifier core runs TLS itself) ships in the slim image
 RUN pip install --no-cache-dir pyyaml python-dateutil requests \
  && useradd --uid 10001 --no-create-home watcher
 WORKDIR /app
