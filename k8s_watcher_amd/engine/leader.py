@@ -266,6 +266,17 @@ class LeaderElector:
         self._set_leader(False)
 
 
+def shard_lease(settings) -> LeaderElectionSettings:
+    """One lease per shard: with ``watcher.shard.count > 1`` the lease name gets a
+    ``-shard-<index>`` suffix, so every shard has its own active replica."""
+    import dataclasses
+    le = settings.watcher.leader_election
+    sh = settings.watcher.shard
+    if sh.count <= 1:
+        return le
+    return dataclasses.replace(le, lease_name=f"{le.lease_name}-shard-{sh.index}")
+
+
 class LeaderElectedService:
     """Run :class:`WatcherService` only while this replica holds the lease.
 
@@ -314,7 +325,7 @@ class LeaderElectedService:
             from ..metrics import start_metrics_server
             metrics_server = await start_metrics_server(self.metrics, self.settings.metrics.host,
                                                         self.settings.metrics.port)
-        self.elector = LeaderElector(api, self.settings.watcher.leader_election, self.metrics)
+        self.elector = LeaderElector(api, shard_lease(self.settings), self.metrics)
         elector_task = asyncio.ensure_future(self.elector.run())
         stopper = asyncio.ensure_future(self._stop.wait())
         try:

@@ -216,3 +216,12 @@ def test_only_leader_notifies_and_standby_takes_over(crash):
         await sink.stop()
         await srv.stop()
     run(body(), timeout=45)
+
+
+def test_one_lease_per_shard():
+    from k8s_watcher_amd.engine.leader import shard_lease
+    s = load_settings("staging", overrides={"watcher": {"shard": {"count": 3, "index": 2},
+                                                        "leader_election": {"enabled": True}}}, environ={})
+    assert shard_lease(s).lease_name == "k8s-watcher-amd-shard-2"
+    s1 = load_settings("staging", overrides={"watcher": {"leader_election": {"enabled": True}}}, environ={})
+    assert shard_lease(s1).lease_name == "k8s-watcher-amd"
