@@ -83,6 +83,8 @@ class EventPipeline:
             self.settings.environment, self.cache, self.metrics.c, self.namespaces or None,
             self.critical_active, self.phase_mode, self.shard.count, self.shard.index, self.shard.by_uid,
             w.event_timestamp == "utc", core, False, False, decode)
+        if w.payload_extra:
+            self.native.set_extra(w.payload_extra)
 
     def handle_raw(self, data: bytes, read_ns: int, framed: bool) -> List[tuple]:
         """Native path: raw watch bytes (HTTP-chunk framed or not) → everything

@@ -167,7 +167,8 @@ class WatcherService:
             self.spool_replayer = SpoolReplayer(self.spool, self.notifier, self.metrics,
                                                 sp.replay_interval_seconds, sp.replay_batch)
             self._tasks.append(asyncio.ensure_future(self.spool_replayer.run()))
-        self.decoder = make_decoder(s.watcher.engine, s.environment, s.watcher.state_format)
+        self.decoder = make_decoder(s.watcher.engine, s.environment, s.watcher.state_format,
+                                    s.watcher.payload_extra)
         scopes = (ShardFilter(s.watcher.shard).namespaces(s.watcher.namespaces)
                   if s.watcher.namespace_scope == "server" and s.watcher.namespaces else [None])
         if s.watcher.shard.count > 1:
@@ -197,7 +198,7 @@ class WatcherService:
             rv = saved_rvs.get(key)
             # Each scope decodes its own stream: give it a private decoder.
             dec = self.decoder if len(scopes) == 1 else make_decoder(
-                s.watcher.engine, s.environment, s.watcher.state_format)
+                s.watcher.engine, s.environment, s.watcher.state_format, s.watcher.payload_extra)
             pipe = self.pipeline if len(scopes) == 1 else self._scope_pipeline(dec)
             self.reflectors.append(Reflector(self.api, s, dec, pipe, self.metrics, namespace=ns,
                                              resource_version=rv, primed=bool(saved_rvs)))

@@ -35,6 +35,28 @@ _STATE_SCHEMA = {
 }
 _STATE_TIME = {"started_at", "finished_at"}
 
+# watcher.payload_extra_fields: opt-in fields the reference does not send
+# (SURVEY §2.3 lists them as missing), emitted as an "extra" object after
+# "metadata", in this order, each as the raw API value or null. Bit i of the
+# mask = EXTRA_FIELDS[i] (the native engine uses the same bits).
+EXTRA_FIELDS = ("pod_ip", "host_ip", "start_time", "qos_class", "resource_version", "owner_references")
+
+
+def extra_mask(names) -> int:
+    mask = 0
+    for n in names or ():
+        if n not in EXTRA_FIELDS:
+            raise ValueError(f"unknown payload extra field {n!r} (choose from {list(EXTRA_FIELDS)})")
+        mask |= 1 << EXTRA_FIELDS.index(n)
+    return mask
+
+
+def _extra(md: Dict[str, Any], st: Optional[Dict[str, Any]], mask: int) -> Dict[str, Any]:
+    st = st if isinstance(st, dict) else {}
+    src = (st.get("podIP"), st.get("hostIP"), st.get("startTime"), st.get("qosClass"),
+           md.get("resourceVersion"), md.get("ownerReferences"))
+    return {name: src[i] for i, name in enumerate(EXTRA_FIELDS) if mask >> i & 1}
+
 
 def _lib_datetime(value: Optional[str]):
     """Parse like the library does (``dateutil.parser.parse``) so reprs match."""
@@ -65,7 +87,8 @@ def container_state_repr(state: Dict[str, Any]) -> str:
 
 
 def build_payload_dict(pod: Dict[str, Any], environment: str, state_format: str = "structured",
-                       event_type: Optional[str] = None, ts_mode: Optional[str] = "local") -> Dict[str, Any]:
+                       event_type: Optional[str] = None, ts_mode: Optional[str] = "local",
+                       extra: int = 0) -> Dict[str, Any]:
     """The reference payload as a dict (``ts_mode=None`` omits ``event_timestamp``)."""
     md = pod.get("metadata") or {}
     st = pod.get("status")
@@ -108,6 +131,8 @@ def build_payload_dict(pod: Dict[str, Any], environment: str, state_format: str 
             "creation_timestamp": k8s_time_to_isoformat(md.get("creationTimestamp")),
         },
     }
+    if extra:
+        out["extra"] = _extra(md, st, extra)
     if ts_mode is not None:
         out["event_timestamp"] = event_timestamp(ts_mode)
     if event_type is not None:
@@ -115,9 +140,9 @@ def build_payload_dict(pod: Dict[str, Any], environment: str, state_format: str 
     return out
 
 
-def build_core(pod: Dict[str, Any], environment: str, state_format: str = "structured") -> bytes:
+def build_core(pod: Dict[str, Any], environment: str, state_format: str = "structured", extra: int = 0) -> bytes:
     """Serialized payload *without* ``event_timestamp``/``event_type`` (ends with ``}``)."""
-    d = build_payload_dict(pod, environment, state_format, None, None)
+    d = build_payload_dict(pod, environment, state_format, None, None, extra)
     return json.dumps(d, ensure_ascii=False, separators=(",", ":")).encode("utf-8")
 
 

@@ -69,7 +69,8 @@ struct Container { Span name, image; };
 
 struct PodSpans {
     bool meta_present = false;
-    Span name, ns, uid, rv, labels, annotations, ctime;
+    Span name, ns, uid, rv, labels, annotations, ctime, owners;
+    Span pod_ip, host_ip, start_time, qos;  // watcher.payload_extra_fields
     bool spec_present = false;
     Span node_name;
     std::vector<Container> containers;
@@ -82,6 +83,7 @@ struct PodSpans {
     void clear() {
         meta_present = spec_present = status_present = deferred = false;
         name = ns = uid = rv = labels = annotations = ctime = node_name = phase = Span();
+        owners = pod_ip = host_ip = start_time = qos = Span();
         spec_raw = cond_raw = cstat_raw = Span();
         containers.clear();
         conditions.clear();
@@ -490,6 +492,7 @@ void parse_metadata(Parser& P, PodSpans& S) {
                 break;
             case 15:
                 if (KEYIS("resourceVersion")) { S.rv = P.value(); return; }
+                if (KEYIS("ownerReferences")) { S.owners = P.value(); return; }
                 break;
             case 17:
                 if (KEYIS("creationTimestamp")) { S.ctime = P.value(); return; }
@@ -561,6 +564,25 @@ void parse_spec(Parser& P, PodSpans& S) {
     });
 }
 
+// status scalars for watcher.payload_extra_fields (a few length-gated compares)
+bool status_scalar(Parser& P, PodSpans& S, const char* k, size_t kn) {
+    switch (kn) {
+        case 5:
+            if (KEYIS("podIP")) { S.pod_ip = P.value(); return true; }
+            break;
+        case 6:
+            if (KEYIS("hostIP")) { S.host_ip = P.value(); return true; }
+            break;
+        case 8:
+            if (KEYIS("qosClass")) { S.qos = P.value(); return true; }
+            break;
+        case 9:
+            if (KEYIS("startTime")) { S.start_time = P.value(); return true; }
+            break;
+    }
+    return false;
+}
+
 void parse_status(Parser& P, PodSpans& S) {
     if (P.null_here()) return;
     S.status_present = true;
@@ -568,7 +590,7 @@ void parse_status(Parser& P, PodSpans& S) {
         if (KEYIS("phase")) S.phase = P.value();
         else if (KEYIS("conditions")) parse_conditions(P, S);
         else if (KEYIS("containerStatuses")) parse_cstatuses(P, S);
-        else P.value();
+        else if (!status_scalar(P, S, k, kn)) P.value();
     });
 }
 
@@ -599,7 +621,7 @@ void parse_status_light(Parser& P, PodSpans& S) {
         if (KEYIS("phase")) S.phase = P.value();
         else if (KEYIS("conditions")) S.cond_raw = P.value();
         else if (KEYIS("containerStatuses")) S.cstat_raw = P.value();
-        else P.value();
+        else if (!status_scalar(P, S, k, kn)) P.value();
     });
 }
 
@@ -758,7 +780,9 @@ void creation_time(std::string& o, const Span& s) {
     o.push_back('"');
 }
 
-void build_core(std::string& o, const PodSpans& S, const std::string& env_json) {
+// extra: bit i = models/payload.py EXTRA_FIELDS[i]
+// (pod_ip, host_ip, start_time, qos_class, resource_version, owner_references)
+void build_core(std::string& o, const PodSpans& S, const std::string& env_json, int extra = 0) {
     o.clear();
     o.append("{\"name\":");
     raw_or_null(o, S.name);
@@ -829,7 +853,25 @@ void build_core(std::string& o, const PodSpans& S, const std::string& env_json) 
     if (falsy_token(S.annotations)) o.append("{}"); else o.append(S.annotations.p, S.annotations.n);
     o.append(",\"creation_timestamp\":");
     creation_time(o, S.ctime);
-    o.append("}}");
+    o.push_back('}');
+    if (extra) {
+        static const char* names[6] = {"pod_ip", "host_ip", "start_time", "qos_class", "resource_version",
+                                       "owner_references"};
+        const Span* vals[6] = {&S.pod_ip, &S.host_ip, &S.start_time, &S.qos, &S.rv, &S.owners};
+        o.append(",\"extra\":{");
+        bool first = true;
+        for (int i = 0; i < 6; ++i) {
+            if (!(extra >> i & 1)) continue;
+            if (!first) o.push_back(',');
+            first = false;
+            o.push_back('"');
+            o.append(names[i]);
+            o.append("\":");
+            raw_or_null(o, *vals[i]);
+        }
+        o.push_back('}');
+    }
+    o.push_back('}');
 }
 
 // ----------------------------------------------------------------------------- Python glue
@@ -974,6 +1016,7 @@ struct DecoderObject {
     size_t cremain;           // bytes left in the current chunk
     long long n_events;
     long long n_bytes;
+    int extra;  // watcher.payload_extra_fields mask
 };
 
 int hexval(char c);
@@ -1059,7 +1102,7 @@ PyObject* event_tuple(DecoderObject* self, int tidx, PyObject* type_obj, const S
             return t;
         }
     } else {
-        build_core(*self->out, S, *self->env_json);
+        build_core(*self->out, S, *self->env_json, self->extra);
         PyObject* core = PyBytes_FromStringAndSize(self->out->data(), (Py_ssize_t)self->out->size());
         if (!core) {
             Py_DECREF(t);
@@ -1456,8 +1499,14 @@ PyObject* Decoder_core_from_summary(DecoderObject* self, PyObject* args) {
         S.status_present = true;
         S.phase = Span{buf[3].data(), buf[3].size()};
     }
-    build_core(*self->out, S, *self->env_json);
+    build_core(*self->out, S, *self->env_json, self->extra);
     return PyBytes_FromStringAndSize(self->out->data(), (Py_ssize_t)self->out->size());
+}
+
+PyObject* Decoder_set_extra(DecoderObject* self, PyObject* arg) {
+    self->extra = (int)PyLong_AsLong(arg);
+    if (PyErr_Occurred()) return nullptr;
+    Py_RETURN_NONE;
 }
 
 PyObject* Decoder_stats(DecoderObject* self, PyObject*) {
@@ -1465,6 +1514,7 @@ PyObject* Decoder_stats(DecoderObject* self, PyObject*) {
 }
 
 PyMethodDef Decoder_methods[] = {
+    {"set_extra", (PyCFunction)Decoder_set_extra, METH_O, "set_extra(mask): watcher.payload_extra_fields"},
     {"feed", (PyCFunction)Decoder_feed, METH_O, "feed(bytes) -> list of event tuples"},
     {"feed_chunked", (PyCFunction)Decoder_feed_chunked, METH_O,
      "feed_chunked(bytes) -> events; input keeps its HTTP chunked framing"},

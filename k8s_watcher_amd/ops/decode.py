@@ -59,9 +59,10 @@ def event_from_object(etype: str, obj: Dict[str, Any]) -> tuple:
 class PyDecoder:
     name = "python"
 
-    def __init__(self, environment: str, state_format: str = "structured") -> None:
+    def __init__(self, environment: str, state_format: str = "structured", extra: int = 0) -> None:
         self.environment = environment
         self.state_format = state_format
+        self.extra = extra
         self._partial = b""
         self._cbuf = b""
         self._cremain = 0
@@ -142,19 +143,20 @@ class PyDecoder:
                 [event_from_object(ADDED, it) for it in items])
 
     def core(self, ev: tuple) -> bytes:
-        return build_core(ev[E_OBJ], self.environment, self.state_format)
+        return build_core(ev[E_OBJ], self.environment, self.state_format, self.extra)
 
     def core_from_summary(self, uid: str, ns: Optional[str], name: Optional[str],
                           phase: Optional[str]) -> bytes:
         pod = {"metadata": {"uid": uid, "namespace": ns, "name": name}}
         if phase is not None:
             pod["status"] = {"phase": phase}
-        return build_core(pod, self.environment, self.state_format)
+        return build_core(pod, self.environment, self.state_format, self.extra)
 
 
-def make_decoder(engine: str, environment: str, state_format: str = "structured"):
-    """``engine="native"`` requires the C++ extension and raises if it is missing."""
+def make_decoder(engine: str, environment: str, state_format: str = "structured", extra: int = 0):
+    """``engine="native"`` requires the C++ extension and raises if it is missing.
+    ``extra`` is a :func:`..models.payload.extra_mask`."""
     if engine == "python" or state_format == "python_repr":
-        return PyDecoder(environment, state_format)
+        return PyDecoder(environment, state_format, extra)
     from .native import NativeDecoder
-    return NativeDecoder(environment, state_format)
+    return NativeDecoder(environment, state_format, extra)

@@ -138,9 +138,12 @@ class NativeDecoder:
 
     name = "native"
 
-    def __init__(self, environment: str, state_format: str = "structured") -> None:
+    def __init__(self, environment: str, state_format: str = "structured", extra: int = 0) -> None:
         mod = load()
         d = mod.StreamDecoder(environment, state_format)
+        if extra:
+            d.set_extra(extra)
+        self.extra = extra
         self._d = d
         self.environment = environment
         self.state_format = state_format

@@ -285,6 +285,7 @@ class WatcherSettings:
     initial_list: str = "notify"  # notify | skip
     initial_sync: str = "list"  # list | watch_list (sendInitialEvents, LIST fallback)
     watch_list_idle_seconds: float = 5.0
+    payload_extra: int = 0  # watcher.payload_extra_fields as a models.payload.extra_mask
     watch_read_bytes: int = 4 << 20  # bytes per socket read on a plain-TCP watch (asyncio default 256 KiB)
     retry: RetryPolicy = field(default_factory=lambda: RetryPolicy(3, 5.0))
     watch_timeout_seconds: int = 300
@@ -348,6 +349,16 @@ def _shard(block: Dict[str, Any]) -> ShardSettings:
     if s.count < 1 or not 0 <= s.index < s.count:
         raise ConfigError(f"watcher.shard: index {s.index} outside [0, {s.count})")
     return s
+
+
+def _payload_extra(names: Any) -> int:
+    from ..models.payload import extra_mask
+    if not isinstance(names, list):
+        raise ConfigError(f"watcher.payload_extra_fields: expected a list, got {names!r}")
+    try:
+        return extra_mask(names)
+    except ValueError as exc:
+        raise ConfigError(f"watcher.payload_extra_fields: {exc}") from None
 
 
 def _spool(block: Dict[str, Any]) -> SpoolSettings:
@@ -430,6 +441,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         initial_list=_choice(w.get("initial_list", "notify"), "watcher.initial_list", ("notify", "skip")),
         initial_sync=_choice(w.get("initial_sync", "list"), "watcher.initial_sync", ("list", "watch_list")),
         watch_list_idle_seconds=_as_float(w.get("watch_list_idle_seconds", 5), "watcher.watch_list_idle_seconds"),
+        payload_extra=_payload_extra(w.get("payload_extra_fields") or []),
         watch_read_bytes=max(0, _as_int(w.get("watch_read_bytes", 4 << 20), "watcher.watch_read_bytes")),
         retry=_retry(w.get("retry"), "watcher.retry", RetryPolicy(3, 5.0), min_attempts=0),
         watch_timeout_seconds=_as_int(w.get("watch_timeout_seconds", 300), "watcher.watch_timeout_seconds"),

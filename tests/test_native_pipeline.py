@@ -198,3 +198,51 @@ def test_decode_pool_create_destroy_race():
             "print('ok')\n") % ROOT
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
     assert out.returncode == 0 and out.stdout.strip() == "ok", out.stderr
+
+
+@pytest.mark.parametrize("mask", [0b111111, 0b010001, 0b100000])
+@pytest.mark.parametrize("env,ov", [("staging", {}), ("production", {})])
+def test_payload_extra_fields_match_python(mask, env, ov):
+    """watcher.payload_extra_fields: the fused pipeline (full and filter-first
+    parse, decode pool) emits the same "extra" object as the Python engine."""
+    from k8s_watcher_amd.models.payload import EXTRA_FIELDS
+    data = stream()
+    s = load_settings(env, overrides=ov, environ={})
+    s.watcher.payload_extra = mask
+    rec_py, rec_nat = Recorder(), Recorder()
+    p = EventPipeline(s, PyDecoder(env, extra=mask), rec_py, Metrics())
+    p.log_events_setting = False
+    p.handle_batch(PyDecoder(env, extra=mask).feed(data), 0)
+    q = EventPipeline(s, PyDecoder(env, extra=mask), rec_nat, Metrics())
+    q.log_events_setting = False
+    q.attach_native()
+    q.handle_raw(data, 0, framed=False)
+    assert rec_py.calls == rec_nat.calls and rec_py.calls
+    want = [n for i, n in enumerate(EXTRA_FIELDS) if mask >> i & 1]
+    for call in rec_nat.calls:
+        assert list(call[4]["extra"]) == want
+    full = [c[4]["extra"] for c in rec_nat.calls if "owner_references" in c[4]["extra"]
+            and c[4]["extra"]["owner_references"]]
+    if mask >> 5 & 1:
+        assert full and full[0]["owner_references"][0]["kind"] == "ReplicaSet"
+
+
+def test_native_decoder_extra_and_config():
+    from k8s_watcher_amd.ops.decode import make_decoder
+    from k8s_watcher_amd.utils.config import ConfigError
+    line = (b'{"type":"ADDED","object":{"metadata":{"name":"a","namespace":"d","uid":"u","resourceVersion":"7",'
+            b'"ownerReferences":[{"kind":"Job","name":"j"}]},"status":{"phase":"Running","podIP":"10.1.2.3",'
+            b'"hostIP":"192.168.0.1","startTime":"2025-01-01T00:00:00Z","qosClass":"BestEffort"}}}\n')
+    cores = [json.loads(make_decoder(e, "staging", extra=0b111111).core(make_decoder(e, "staging", extra=0b111111)
+                                                                          .feed(line)[0])) for e in ("python",)]
+    d = make_decoder("native", "staging", extra=0b111111)
+    nat = json.loads(d.core(d.feed(line)[0]))
+    assert nat == cores[0]
+    assert nat["extra"] == {"pod_ip": "10.1.2.3", "host_ip": "192.168.0.1", "start_time": "2025-01-01T00:00:00Z",
+                            "qos_class": "BestEffort", "resource_version": "7",
+                            "owner_references": [{"kind": "Job", "name": "j"}]}
+    s = load_settings("staging", overrides={"watcher": {"payload_extra_fields": ["pod_ip", "owner_references"]}},
+                      environ={})
+    assert s.watcher.payload_extra == 0b100001
+    with pytest.raises(ConfigError):
+        load_settings("staging", overrides={"watcher": {"payload_extra_fields": ["nope"]}}, environ={})

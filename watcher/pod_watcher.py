@@ -104,6 +104,7 @@ class PodWatcher:
     # ------------------------------------------------------------------ per event
     def _extract_pod_data(self, pod: Any) -> Dict[str, Any]:
         return build_payload_dict(raw_of(pod), self.environment, self.settings.watcher.state_format,
+                                  extra=self.settings.watcher.payload_extra,
                                   ts_mode=self.settings.watcher.event_timestamp)
 
     def should_process_event(self, event_type: str, pod: Any) -> bool:
