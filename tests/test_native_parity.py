@@ -228,3 +228,25 @@ def test_fuzz_block_skipper_all_levels(skipme, pad):
         mod.set_simd(True)
     assert out[0] == out[1] == out[2]
     assert out[0] and out[0][0][0] == "MODIFIED"
+
+
+pod_extra = st.fixed_dictionaries({}, optional={
+    "metadata": maybe(st.fixed_dictionaries({}, optional={
+        "name": scalar, "uid": scalar, "resourceVersion": scalar,
+        "ownerReferences": maybe(st.lists(st.dictionaries(text, scalar, max_size=3), max_size=2))})),
+    "status": maybe(st.fixed_dictionaries({}, optional={
+        "phase": scalar, "podIP": scalar, "hostIP": scalar, "startTime": scalar, "qosClass": scalar,
+        "conditions": maybe(st.lists(st.fixed_dictionaries({}, optional={"type": scalar}), max_size=2))})),
+})
+
+
+@settings(max_examples=200, deadline=None)
+@given(obj=pod_extra, mask=st.integers(0, 63), ascii_=st.booleans())
+def test_fuzz_extra_fields_parity(obj, mask, ascii_):
+    """watcher.payload_extra_fields: same "extra" object from both engines for any mask."""
+    from k8s_watcher_amd.ops.decode import PyDecoder
+    from k8s_watcher_amd.ops.native import NativeDecoder
+    line = json.dumps({"type": "MODIFIED", "object": obj}, ensure_ascii=ascii_).encode("utf-8") + b"\n"
+    py, nat = PyDecoder("staging", extra=mask), NativeDecoder("staging", extra=mask)
+    x, y = py.feed(line)[0], nat.feed(line)[0]
+    assert json.loads(py.core(x)) == json.loads(nat.core(y))
