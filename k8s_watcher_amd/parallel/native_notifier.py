@@ -82,7 +82,8 @@ class NativeNotifierPool:
             self.core.set_rate_limit(settings.rate_limit_qps, settings.rate_limit_burst)
         self._throttle_timer: Optional[asyncio.TimerHandle] = None
         if self.tls:  # TLS runs inside the core (OpenSSL on the same non-blocking sockets)
-            self.core.enable_tls(self.host, settings.ca_file, settings.verify_tls)
+            self.core.enable_tls(self.host, settings.ca_file, settings.verify_tls, settings.cert_file,
+                                 settings.key_file)
         self.n = settings.pool.connections
         self.socks: Dict[int, socket.socket] = {}
         self.connecting: set = set()
@@ -161,6 +162,8 @@ class NativeNotifierPool:
             return None
         import ssl
         ctx = ssl.create_default_context(cafile=self.settings.ca_file)
+        if self.settings.cert_file:
+            ctx.load_cert_chain(self.settings.cert_file, self.settings.key_file)
         if not self.settings.verify_tls:
             ctx.check_hostname = False
             ctx.verify_mode = ssl.CERT_NONE

@@ -226,6 +226,8 @@ class NotifierPool:
         if u.scheme == "https" and ssl_context is None:
             import ssl
             ssl_context = ssl.create_default_context(cafile=settings.ca_file)
+            if settings.cert_file:  # mutual TLS
+                ssl_context.load_cert_chain(settings.cert_file, settings.key_file)
             if not settings.verify_tls:
                 ssl_context.check_hostname = False
                 ssl_context.verify_mode = ssl.CERT_NONE

@@ -238,6 +238,8 @@ class ClusterApiSettings:
     pool: NotifierPoolSettings = field(default_factory=NotifierPoolSettings)
     verify_tls: bool = True
     ca_file: Optional[str] = None
+    cert_file: Optional[str] = None  # client certificate for mutual TLS (with key_file)
+    key_file: Optional[str] = None
     health_check_on_start: bool = True
     spool: SpoolSettings = field(default_factory=SpoolSettings)
     rate_limit_qps: float = 0.0  # clusterapi.rate_limit.qps; 0 = unlimited
@@ -483,6 +485,8 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         ),
         verify_tls=_as_bool(c.get("verify_tls", True), "clusterapi.verify_tls"),
         ca_file=c.get("ca_file") or None,
+        cert_file=c.get("cert_file") or None,
+        key_file=c.get("key_file") or None,
         health_check_on_start=_as_bool(c.get("health_check_on_start", True), "clusterapi.health_check_on_start"),
         spool=_spool(c.get("spool") or {}),
         rate_limit_qps=max(0.0, _as_float((c.get("rate_limit") or {}).get("qps", 0), "clusterapi.rate_limit.qps")),

@@ -118,3 +118,29 @@ def test_service_uses_native_core_for_https(pki):
         await sink.stop()
         await srv.stop()
     run(body())
+
+
+@pytest.mark.parametrize("with_cert", [True, False])
+def test_mutual_tls(pool_cls, pki, with_cert):
+    """clusterapi.cert_file/key_file: a sink that requires a client certificate
+    accepts the pool only when it presents one signed by the CA."""
+    async def body():
+        ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+        ctx.load_cert_chain(pki.server_crt, pki.server_key)
+        ctx.load_verify_locations(pki.ca_crt)
+        ctx.verify_mode = ssl.CERT_REQUIRED
+        sink = StubSink()
+        await sink.start(ssl_context=ctx)
+        m = Metrics()
+        kw = {"cert_file": pki.client_crt, "key_file": pki.client_key} if with_cert else {}
+        pool = pool_cls(settings(sink.url, ca_file=pki.ca_crt, attempts=1, **kw), m)
+        pool.submit("u", "ADDED", "default", "p", core("u"), 0, TS)
+        pool.flush()
+        assert await pool.drain(10)
+        if with_cert:
+            assert m.c["notify_delivered"] == 1 and sink.state.count == 1
+        else:
+            assert m.c["notify_failed"] == 1 and sink.state.count == 0
+        await pool.close()
+        await sink.stop()
+    run(body())
