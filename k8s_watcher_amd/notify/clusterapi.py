@@ -32,8 +32,10 @@ RETRYABLE = frozenset({408, 425, 429, 500, 502, 503, 504})
 class _Common:
     def __init__(self, base_url: str, api_key: Optional[str] = None, timeout: float = 30.0,
                  pod_update: str = "/api/pods/update", health: str = "/health",
-                 retry: Optional[RetryPolicy] = None) -> None:
+                 retry: Optional[RetryPolicy] = None, verify_tls: bool = True, ca_file: Optional[str] = None,
+                 cert_file: Optional[str] = None, key_file: Optional[str] = None) -> None:
         self.base_url = base_url.rstrip("/")
+        self.verify_tls, self.ca_file, self.cert_file, self.key_file = verify_tls, ca_file, cert_file, key_file
         self.api_key = api_key
         self.timeout = timeout
         self.pod_update = pod_update
@@ -50,7 +52,8 @@ class _Common:
 
     @classmethod
     def from_settings(cls, c) -> "_Common":
-        return cls(c.base_url, c.api_key or None, c.timeout, c.pod_update, c.health, c.retry)
+        return cls(c.base_url, c.api_key or None, c.timeout, c.pod_update, c.health, c.retry,
+                   verify_tls=c.verify_tls, ca_file=c.ca_file, cert_file=c.cert_file, key_file=c.key_file)
 
 
 class ClusterApiClient(_Common):
@@ -62,6 +65,10 @@ class ClusterApiClient(_Common):
         self._requests = requests
         self.session = requests.Session()
         self.session.headers.update(self.headers)
+        # per request: a session-level ``verify`` loses to $REQUESTS_CA_BUNDLE in requests
+        self._tls_kw: Dict[str, Any] = {"verify": self.ca_file or self.verify_tls}
+        if self.cert_file:
+            self._tls_kw["cert"] = (self.cert_file, self.key_file) if self.key_file else self.cert_file
 
     def update_pod_status(self, pod_data: Dict[str, Any]) -> bool:
         ep = self.endpoint
@@ -72,7 +79,7 @@ class ClusterApiClient(_Common):
         for attempt in range(1, max(1, self.retry.max_attempts) + 1):
             status = None
             try:
-                resp = self.session.post(ep, data=body, timeout=self.timeout)
+                resp = self.session.post(ep, data=body, timeout=self.timeout, **self._tls_kw)
                 status = resp.status_code
                 if 200 <= status < 300:
                     self.logger.info(f"Successfully updated pod data for {pod_data.get('name', 'unknown')}")
@@ -93,7 +100,7 @@ class ClusterApiClient(_Common):
 
     def health_check(self) -> bool:
         try:
-            resp = self.session.get(f"{self.base_url}{self.health}", timeout=min(5.0, self.timeout))
+            resp = self.session.get(f"{self.base_url}{self.health}", timeout=min(5.0, self.timeout), **self._tls_kw)
             return 200 <= resp.status_code < 300
         except Exception:  # noqa: BLE001 - parity: any failure -> False
             return False
@@ -104,6 +111,14 @@ class AsyncClusterApiClient(_Common):
 
     def __init__(self, *args: Any, ssl_context=None, **kwargs: Any) -> None:
         super().__init__(*args, **kwargs)
+        if ssl_context is None and self.base_url.startswith("https://"):
+            import ssl
+            ssl_context = ssl.create_default_context(cafile=self.ca_file)
+            if self.cert_file:
+                ssl_context.load_cert_chain(self.cert_file, self.key_file)
+            if not self.verify_tls:
+                ssl_context.check_hostname = False
+                ssl_context.verify_mode = ssl.CERT_NONE
         self.http = HttpClient(self.base_url, ssl_context, headers=self.headers, timeout=self.timeout)
 
     async def update_pod_status(self, pod_data: Dict[str, Any]) -> bool:

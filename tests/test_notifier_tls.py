@@ -144,3 +144,32 @@ def test_mutual_tls(pool_cls, pki, with_cert):
         await pool.close()
         await sink.stop()
     run(body())
+
+
+def test_compat_clients_over_mutual_tls(pki):
+    """The reference-compatible clients (sync and async) honour the same TLS settings."""
+    import threading
+    from k8s_watcher_amd.notify.clusterapi import AsyncClusterApiClient, ClusterApiClient
+    from k8s_watcher_amd.testing.stub_sink import StubSink as _Sink
+
+    async def body():
+        ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+        ctx.load_cert_chain(pki.server_crt, pki.server_key)
+        ctx.load_verify_locations(pki.ca_crt)
+        ctx.verify_mode = ssl.CERT_REQUIRED
+        sink = _Sink()
+        await sink.start(ssl_context=ctx)
+        s = settings(sink.url, ca_file=pki.ca_crt, cert_file=pki.client_crt, key_file=pki.client_key)
+        ac = AsyncClusterApiClient.from_settings(s)
+        assert await ac.update_pod_status({"name": "a", "uid": "1"})
+        sc = ClusterApiClient.from_settings(s)
+        out = {}
+        t = threading.Thread(target=lambda: out.update(ok=sc.update_pod_status({"name": "b", "uid": "2"}),
+                                                       health=sc.health_check()))
+        t.start()
+        while t.is_alive():
+            await asyncio.sleep(0.01)
+        assert out == {"ok": True, "health": True}
+        assert sink.state.count == 2
+        await sink.stop()
+    run(body())
