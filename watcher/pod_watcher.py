@@ -155,6 +155,9 @@ class PodWatcher:
 
         async def run() -> None:
             svc = WatcherService(self.settings)
+            if self.settings.watcher.leader_election.enabled:  # one active replica of several
+                from k8s_watcher_amd.engine.leader import LeaderElectedService
+                svc = LeaderElectedService(self.settings)
             loop = asyncio.get_running_loop()
             for sig in (signal.SIGINT, signal.SIGTERM):
                 try:
