@@ -52,6 +52,8 @@ async def _run_service(settings, check_only: bool) -> int:
         svc = LeaderElectedService(settings)
     if check_only:
         ok = await svc.setup_k8s_client()
+        if ok:
+            ok = await svc.preflight()
         if svc.api is not None:
             await svc.api.close()
         return 0 if ok else 1

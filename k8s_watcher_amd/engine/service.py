@@ -119,6 +119,50 @@ class WatcherService:
             self.api = None
         return False
 
+    async def preflight(self) -> bool:
+        """``--check``: the RBAC permissions this configuration needs (SelfSubjectAccessReview)
+        and the clusterapi health endpoint. Logs one line per item; True if all pass."""
+        assert self.api is not None
+        s = self.settings
+        wanted = []
+        scopes = s.watcher.namespaces if s.watcher.namespace_scope == "server" and s.watcher.namespaces else [None]
+        for ns in scopes:
+            wanted += [("list", "pods", "", ns, None), ("watch", "pods", "", ns, None)]
+        wanted.append(("list", "namespaces", "", None, None))
+        le = s.watcher.leader_election
+        if le.enabled:
+            from .leader import default_lease_namespace, shard_lease
+            lease = shard_lease(s)
+            ns = lease.lease_namespace or default_lease_namespace()
+            wanted += [("get", "leases", "coordination.k8s.io", ns, lease.lease_name),
+                       ("update", "leases", "coordination.k8s.io", ns, lease.lease_name),
+                       ("create", "leases", "coordination.k8s.io", ns, None)]
+        ok = True
+        for verb, res, group, ns, name in wanted:
+            what = f"{verb} {group + '/' if group else ''}{res}" + (f" in {ns}" if ns else " (cluster-wide)")
+            try:
+                allowed, reason = await self.api.can_i(verb, res, group, ns, name)
+            except (ApiError, HttpError) as exc:
+                self.log.warning(f"Permission check for {what} unavailable: {exc}")
+                continue
+            if allowed:
+                self.log.info(f"Permission OK: {what}")
+            else:
+                ok = False
+                self.log.error(f"Permission missing: {what}" + (f" ({reason})" if reason else ""))
+        if s.clusterapi.enabled:
+            self.event_log = EventLog(self.log)
+            notifier = self._make_notifier()
+            try:
+                if await notifier.health_check():
+                    self.log.info(f"ClusterAPI health check passed: {s.clusterapi.base_url}{s.clusterapi.health}")
+                else:
+                    ok = False
+                    self.log.error(f"ClusterAPI health check failed: {s.clusterapi.base_url}{s.clusterapi.health}")
+            finally:
+                await notifier.close()
+        return ok
+
     def _make_notifier(self):
         c = self.settings.clusterapi
         w = self.settings.watcher

@@ -154,6 +154,21 @@ class KubeApi:
         """PUT; ``metadata.resourceVersion`` in ``lease`` makes it a compare-and-swap (409 on conflict)."""
         return await self._json("PUT", lease_path(namespace, name), lease, timeout)
 
+    # ------------------------------------------------------------------ authorization.k8s.io/v1
+    async def can_i(self, verb: str, resource: str, group: str = "", namespace: Optional[str] = None,
+                    name: Optional[str] = None, timeout: Optional[float] = None) -> Tuple[bool, str]:
+        """SelfSubjectAccessReview: may this identity ``verb`` the ``resource``? -> (allowed, reason)."""
+        attrs: Dict[str, object] = {"verb": verb, "resource": resource, "group": group}
+        if namespace:
+            attrs["namespace"] = namespace
+        if name:
+            attrs["name"] = name
+        doc = await self._json("POST", "/apis/authorization.k8s.io/v1/selfsubjectaccessreviews",
+                               {"apiVersion": "authorization.k8s.io/v1", "kind": "SelfSubjectAccessReview",
+                                "spec": {"resourceAttributes": attrs}}, timeout)
+        st = doc.get("status") or {}
+        return bool(st.get("allowed")), str(st.get("reason") or "")
+
     async def close(self) -> None:
         await self.http.close()
 

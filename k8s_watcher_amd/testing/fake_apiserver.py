@@ -155,6 +155,7 @@ class FakeApiServer:
         self.loop: Optional[asyncio.AbstractEventLoop] = None
         self._bm_task: Optional[asyncio.Task] = None
         self.gzipped_responses = 0
+        self.denied: Set[Tuple[str, str]] = set()  # (verb, resource) the fake RBAC refuses
         self.leases: Dict[Tuple[str, str], Dict[str, Any]] = {}
         self.lease_writes: List[Tuple[Tuple[str, str], Dict[str, Any]]] = []
         self.lease_fault: Optional[int] = None  # answer every lease request with this status
@@ -364,6 +365,18 @@ class FakeApiServer:
                 self.fail_next.pop(0)
                 self._send_json(writer, st, _status(st, "InternalError", "injected failure"), "Injected")
                 return True
+        if path == "/apis/authorization.k8s.io/v1/selfsubjectaccessreviews" and method == "POST":
+            try:
+                attrs = (json.loads(body).get("spec") or {}).get("resourceAttributes") or {}
+            except ValueError:
+                attrs = {}
+            key = (attrs.get("verb"), attrs.get("resource"))
+            allowed = key not in self.denied
+            doc = {"apiVersion": "authorization.k8s.io/v1", "kind": "SelfSubjectAccessReview",
+                   "spec": {"resourceAttributes": attrs},
+                   "status": {"allowed": allowed, **({} if allowed else {"reason": "denied by the fake RBAC"})}}
+            self._send_json(writer, 201, doc, "Created")
+            return True
         if path.startswith(LEASES_PREFIX):
             code, doc = self._lease(method, path[len(LEASES_PREFIX):], body)
             self._send_json(writer, code, doc, _REASONS.get(code, "OK"))

@@ -93,6 +93,17 @@ def test_check_mode(cluster):
     assert r.returncode == 0, r.stderr
     assert "Successfully connected to Kubernetes API version: v1.33.1-fake" in r.stderr
     assert "Sample namespaces: ['default', 'kube-system']" in r.stderr
+    assert "Permission OK: watch pods (cluster-wide)" in r.stderr
+
+
+def test_check_mode_reports_missing_rbac(cluster):
+    st, srv, cfg = cluster
+    srv.denied.add(("watch", "pods"))
+    r = cli("staging", "--config-dir", cfg, "--check", "--set", "watcher.leader_election.enabled=true",
+            "--set", "watcher.leader_election.lease_namespace=ops")
+    assert r.returncode == 1, r.stderr
+    assert "Permission missing: watch pods (cluster-wide) (denied by the fake RBAC)" in r.stderr
+    assert "Permission OK: update coordination.k8s.io/leases in ops" in r.stderr
 
 
 def test_sigterm_graceful_shutdown(cluster):
