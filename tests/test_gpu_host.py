@@ -40,3 +40,22 @@ def test_bench_line_is_valid():
         assert key in line
     assert line["value"] > 0 and line["n_gpus"] == 1 and line["steps"] == 2
     assert line["notify_failed"] == 0
+
+
+def test_tls_bench_line_is_valid():
+    """production.yaml's https clusterapi through the native TLS notifier core, on the host."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                          "--pods-per-step", "1000", "--ref-events", "0", "--latency-seconds", "1", "--tls"],
+                         capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["config"]["clusterapi"] == "https" and line["value"] > 0 and line["notify_failed"] == 0
+
+
+def test_sharded_ha_and_spool_paths_on_host(tmp_path):
+    """Leader election + spool + checkpoint together on the deployment host's CPUs."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import test_ha_soak
+    import test_spool
+    test_ha_soak.test_graceful_handover_under_churn_keeps_final_state(tmp_path / "ha")
+    test_spool.test_shutdown_with_owed_notifications_spools_then_checkpoints(tmp_path / "sp")
