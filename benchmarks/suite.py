@@ -105,14 +105,18 @@ class Servers:
                 pass
         for p in (self.replay, self.sink):
             try:
-                await asyncio.wait_for(p.wait(), 10)
+                await asyncio.wait_for(p.wait(), 300 if (self.verify_dir and p is self.sink) else 10)
             except asyncio.TimeoutError:
                 os.killpg(p.pid, signal.SIGKILL)
             t = getattr(p, "_transport", None)
             if t is not None:
                 t.close()
         if self.verify_dir:
-            await asyncio.sleep(0.5)  # workers write their dumps on SIGTERM
+            # every worker writes its dump on SIGTERM (renamed into place when complete)
+            deadline = time.monotonic() + 300
+            while (len(glob.glob(os.path.join(self.verify_dir, "sink-*.json"))) < self.sink_workers
+                   and time.monotonic() < deadline):
+                await asyncio.sleep(0.1)
 
 
 async def run_ours(srv: Servers, profile: str, overrides: dict, steps: List[str], warm_steps: List[str],
@@ -172,6 +176,9 @@ async def run_ours(srv: Servers, profile: str, overrides: dict, steps: List[str]
         out.update({"p50_ms": p50 / 1e6 if p50 else None, "p99_ms": p99 / 1e6 if p99 else None,
                     "latency_samples": m.latency.n})
     out["counters"] = {k: v for k, v in c.items() if v}
+    import resource
+    out["max_rss_mb"] = round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024, 1)  # watcher process
+    out["cached_pods_at_end"] = len(svc.pipeline.cache) if svc.pipeline is not None else None
     svc.stop()
     await svc.shutdown()
     return out

@@ -263,8 +263,10 @@ def run_sink_process(port: int, workers: int = 1, latency: float = 0.0,
         await stop.wait()
         if verify_dir:
             st = sink.state
-            with open(os.path.join(verify_dir, f"sink-{os.getpid()}.json"), "w") as fh:
+            final = os.path.join(verify_dir, f"sink-{os.getpid()}.json")
+            with open(final + ".tmp", "w") as fh:  # renamed when complete: readers never see a partial dump
                 json.dump({"count": st.count, "keys": {k.decode(): v for k, v in st.keys.items()}}, fh)
+            os.replace(final + ".tmp", final)
 
     try:
         asyncio.run(serve())
