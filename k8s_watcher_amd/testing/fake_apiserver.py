@@ -611,6 +611,34 @@ class ServerThread:
         self.thread.join(5)
 
 
+async def replay_capture(srv: FakeApiServer, events: List[dict], speed: float = 1.0) -> int:
+    """Apply captured watch events (``tools/capture.py``) at ``speed`` x the recorded pace
+    (0 = as fast as possible). Each event is re-stamped with this server's resourceVersions."""
+    loop = asyncio.get_running_loop()
+    t0 = loop.time()
+    n = 0
+    for r in events:
+        if speed > 0:
+            delay = t0 + r["t"] / speed - loop.time()
+            if delay > 0:
+                await asyncio.sleep(delay)
+        obj = r["object"]
+        md = obj.get("metadata") or {}
+        key = (md.get("namespace", "default"), md.get("name"))
+        et = r["type"]
+        if et == "ADDED" and key in srv.pods:
+            et = "MODIFIED"  # a capture that starts mid-watch may repeat an ADDED
+        elif et == "MODIFIED" and key not in srv.pods:
+            et = "ADDED"
+        elif et == "DELETED" and key not in srv.pods:
+            continue
+        srv.apply(et, obj)
+        n += 1
+        if speed <= 0 and n % 512 == 0:
+            await asyncio.sleep(0)
+    return n
+
+
 def main(argv: Optional[List[str]] = None) -> None:
     ap = argparse.ArgumentParser(description="fake kube-apiserver for k8s-watcher")
     ap.add_argument("--host", default="127.0.0.1")
@@ -618,12 +646,25 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--token", default=None)
     ap.add_argument("--pods", type=int, default=10, help="pods to pre-create")
     ap.add_argument("--churn-rate", type=float, default=0.0, help="lifecycle events/s after start")
+    ap.add_argument("--replay", default=None, help="serve a capture (k8s_watcher_amd.tools.capture)")
+    ap.add_argument("--speed", type=float, default=1.0, help="replay pace: 1 = as recorded, 0 = flat out")
     args = ap.parse_args(argv)
 
     from .podgen import PodFactory, churn_events
 
     async def run() -> None:
         srv = FakeApiServer(token=args.token, bookmark_interval=30)
+        if args.replay:
+            from ..tools.capture import load_capture
+            records = load_capture(args.replay)
+            for r in records:
+                if r["type"] == "LIST":
+                    srv.create(r["object"])
+            port = await srv.start(args.host, args.port)
+            print(f"fake kube-apiserver listening on http://{args.host}:{port} (replaying {args.replay})",
+                  flush=True)
+            await replay_capture(srv, [r for r in records if r["type"] != "LIST"], args.speed)
+            await asyncio.Event().wait()
         f = PodFactory(seed=1, namespaces=["default", "kube-system", "production", "monitoring"])
         for _ in range(args.pods):
             srv.create(f.running(f.new_pod()))
