@@ -379,14 +379,17 @@ class LeaderElectedService:
 
     async def _end_term(self, svc, run: "asyncio.Future", graceful: bool) -> None:
         # graceful (SIGTERM while leading): drain and checkpoint as a lone
-        # watcher would; lease lost: abandon the queue, leave the checkpoint alone
-        await svc.shutdown(drain_timeout=10.0 if graceful else 0.0, checkpoint=graceful)
-        if not run.done():
+        # watcher would; lease lost: abandon the queue, leave the checkpoint alone.
+        # The term's task ends first (svc.stop() was called; a lost lease also
+        # cancels it), so a start() still in progress cannot create reflectors
+        # after the shutdown below.
+        if not graceful and not run.done():
             run.cancel()
         try:
             await run
         except (asyncio.CancelledError, Exception):  # noqa: BLE001 - the term is over either way
             pass
+        await svc.shutdown(drain_timeout=10.0 if graceful else 0.0, checkpoint=graceful)
 
 
 class LeadershipLost(Exception):
