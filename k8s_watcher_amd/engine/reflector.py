@@ -42,6 +42,9 @@ from ..utils.config import Settings
 from ..utils.logsetup import SERVICE_LOGGER
 from .pipeline import EventPipeline
 
+# a watch that ends sooner than this without moving the resourceVersion is
+# treated like client-go's "very short watch": back off before reconnecting
+SHORT_WATCH_SECONDS = 1.0
 
 class Expired(Exception):
     """The watch resourceVersion is too old (410 Gone)."""
@@ -326,11 +329,21 @@ class Reflector:
                     first = False
                 else:
                     self.synced.set()
+                rv_before, t0 = self.rv, time.monotonic()
                 await self.watch_once()
+                if self._stop.is_set():
+                    break
+                self.metrics.c["watch_restarts"] += 1
+                if time.monotonic() - t0 < SHORT_WATCH_SECONDS and self.rv == rv_before:
+                    # the server ended the watch at once with nothing in it
+                    # (proxy or API server misbehaving): back off instead of
+                    # reconnecting in a hot loop. Not a failure for
+                    # max_attempts — the connection itself worked.
+                    self.metrics.c["short_watches"] += 1
+                    await self._sleep(backoff.next_delay())
+                    continue
                 failures = 0
                 backoff.reset()
-                if not self._stop.is_set():
-                    self.metrics.c["watch_restarts"] += 1
             except Expired:
                 self.metrics.c["expired_410"] += 1
                 self.log.warning(f"Watch resourceVersion {self.rv} expired (410); relisting")
@@ -358,6 +371,10 @@ class Reflector:
         delay = backoff.next_delay()
         self.log.warning(f"Watch failed ({exc}); retry {failures}/{limit or 'inf'} in {delay:.2f}s")
         self.metrics.c["watch_restarts"] += 1
+        await self._sleep(delay)
+
+    async def _sleep(self, delay: float) -> None:
+        """Sleep ``delay`` seconds or until :meth:`stop`."""
         waiter = asyncio.ensure_future(self._stop.wait())
         try:
             await asyncio.wait([waiter], timeout=delay)

@@ -39,6 +39,7 @@ COUNTERS = (
     "spool_stale_skipped",
     "spool_dropped",
     "watch_restarts",
+    "short_watches",        # watches the server ended at once with nothing in them (backed off)
     "relists",
     "watch_list_syncs",     # initial state via WatchList (sendInitialEvents) instead of LIST
     "expired_410",

@@ -149,6 +149,7 @@ class FakeApiServer:
         self.watches: Set[_Watch] = set()
         self.writers: Set[asyncio.StreamWriter] = set()
         self.fail_next: List[Tuple[int, str]] = []
+        self.empty_watches = 0
         self.requests: List[Tuple[str, str]] = []
         self.server: Optional[asyncio.AbstractServer] = None
         self.port = 0
@@ -303,6 +304,11 @@ class FakeApiServer:
     def fail_requests(self, n: int, status: int = 500, path_prefix: str = "") -> None:
         for _ in range(n):
             self.fail_next.append((status, path_prefix))
+
+    def hang_up_watches(self, n: int) -> None:
+        """The next ``n`` watches get a 200 with an empty body that ends at once
+        (a proxy that closes every watch); backlog events are not sent."""
+        self.empty_watches += n
 
     # ------------------------------------------------------------------ HTTP
     async def _handle(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
@@ -484,6 +490,12 @@ class FakeApiServer:
         w = _Watch(writer, ns, q.get("labelSelector"), q.get("fieldSelector"),
                    q.get("allowWatchBookmarks") in ("true", "1"))
         rv_param = q.get("resourceVersion")
+        if self.empty_watches > 0:
+            self.empty_watches -= 1
+            writer.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\n"
+                         b"Transfer-Encoding: chunked\r\n\r\n0\r\n\r\n")
+            await writer.drain()
+            return
         if q.get("sendInitialEvents") in ("true", "1"):
             await self._watch_list(writer, w, q)
             return

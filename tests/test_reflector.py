@@ -3,6 +3,7 @@ bookmarks, retries, checkpoint restart — each asserting exactly-once delivery.
 
 import asyncio
 import collections
+import time
 
 import pytest
 
@@ -178,6 +179,27 @@ def test_retry_budget_exhausted_is_fatal():
             st.srv.drop_connections()
             with pytest.raises(WatchFailed):
                 await asyncio.wait_for(svc.wait(), 10)
+
+    run(body())
+
+
+def test_short_watches_back_off_without_failing():
+    # a proxy that ends every watch at once: reconnects are paced by the
+    # backoff (no hot loop) and do not spend the failure budget
+    async def body():
+        async with Stack() as st:
+            st.srv.hang_up_watches(4)
+            svc = st.service({"watcher": {"retry": {"delay_seconds": 0.05, "max_attempts": 2}}})
+            t0 = time.monotonic()
+            await svc.start()
+            evs = lifecycle_apply(st, 2)
+            await st.settle(len(evs))
+            assert_exactly_once(st.delivered(), evs)
+            assert svc.metrics.c["short_watches"] == 4
+            assert time.monotonic() - t0 >= 0.05 * 4 * 0.5  # backed off between reconnects
+            watches = [t for m, t in st.srv.requests if "watch=" in t]
+            assert len(watches) == 5
+            assert not any(t.done() for t in svc._tasks)  # the watch did not give up
 
     run(body())
 
