@@ -49,7 +49,8 @@ class KubeApi:
         headers = {"Accept": "application/json", "User-Agent": USER_AGENT}
         headers.update(endpoint.static_headers)
         self.http = HttpClient(endpoint.server, endpoint.ssl_context, headers=headers,
-                               timeout=timeout, header_provider=endpoint.header_provider)
+                               timeout=timeout, header_provider=endpoint.header_provider,
+                               server_name=endpoint.tls_server_name)
 
     async def _get(self, path: str, query: Optional[Dict[str, object]] = None,
                    timeout: Optional[float] = None, headers: Optional[Dict[str, str]] = None) -> Response:

@@ -50,6 +50,7 @@ class KubeEndpoint:
     namespace: Optional[str] = None
     source: str = ""
     context_name: Optional[str] = None
+    tls_server_name: Optional[str] = None  # verify the server certificate against this name
 
     def auth_headers(self) -> Dict[str, str]:
         h = dict(self.static_headers)
@@ -161,7 +162,7 @@ def _load_cert_chain(ctx: ssl.SSLContext, cert_pem: bytes, key_pem: bytes) -> No
 
 def build_ssl_context(ca_file: Optional[str] = None, ca_data: Optional[bytes] = None,
                       insecure: bool = False, cert_pem: Optional[bytes] = None,
-                      key_pem: Optional[bytes] = None, server_name: Optional[str] = None) -> ssl.SSLContext:
+                      key_pem: Optional[bytes] = None) -> ssl.SSLContext:
     if insecure:
         ctx = ssl.create_default_context()
         ctx.check_hostname = False
@@ -173,16 +174,15 @@ def build_ssl_context(ca_file: Optional[str] = None, ca_data: Optional[bytes] = 
         ctx = ssl.create_default_context()
     if cert_pem and key_pem:
         _load_cert_chain(ctx, cert_pem, key_pem)
-    if server_name:
-        ctx.check_hostname = False  # hostname checked against tls-server-name is not expressible; trust the CA
     return ctx
 
 
 class _ExecCredential:
     """Runs a client-go ``exec`` credential plugin and caches its token."""
 
-    def __init__(self, spec: Dict[str, Any]) -> None:
+    def __init__(self, spec: Dict[str, Any], base: str = "") -> None:
         self.spec = spec
+        self.base = base  # a relative command path resolves against the kubeconfig's directory
         self._token: Optional[str] = None
         self._expiry: float = 0.0
 
@@ -196,9 +196,12 @@ class _ExecCredential:
         cmd = [self.spec.get("command")] + list(self.spec.get("args") or [])
         if not cmd[0]:
             raise ConfigException("exec credential plugin has no command")
+        if self.base and os.sep in cmd[0] and not os.path.isabs(cmd[0]):
+            cmd[0] = os.path.join(self.base, cmd[0])
         env = dict(os.environ)
         for item in self.spec.get("env") or []:
-            env[item["name"]] = item["value"]
+            if isinstance(item, dict) and item.get("name"):
+                env[item["name"]] = str(item.get("value", ""))
         api_version = self.spec.get("apiVersion", "client.authentication.k8s.io/v1beta1")
         env["KUBERNETES_EXEC_INFO"] = json.dumps(
             {"apiVersion": api_version, "kind": "ExecCredential", "spec": {"interactive": False}})
@@ -278,7 +281,7 @@ def load_kube_config(config_file: Optional[str] = None, context: Optional[str] =
     elif user.get("tokenFile"):
         provider = _TokenFile(_resolve(ubase, user["tokenFile"])).headers  # type: ignore[arg-type]
     elif user.get("exec"):
-        provider = _ExecCredential(user["exec"]).headers
+        provider = _ExecCredential(user["exec"], ubase).headers
     elif user.get("username") and user.get("password"):
         cred = base64.b64encode(f"{user['username']}:{user['password']}".encode()).decode()
         headers["Authorization"] = f"Basic {cred}"
@@ -302,13 +305,13 @@ def load_kube_config(config_file: Optional[str] = None, context: Optional[str] =
                 ca_file=_resolve(cbase, cluster.get("certificate-authority")),
                 ca_data=ca_data,
                 insecure=bool(cluster.get("insecure-skip-tls-verify")),
-                cert_pem=cert, key_pem=key,
-                server_name=cluster.get("tls-server-name"))
+                cert_pem=cert, key_pem=key)
         except (ssl.SSLError, OSError, ValueError) as exc:
             raise ConfigException(f"TLS setup for cluster {cluster_name!r} failed: {exc}") from None
     return KubeEndpoint(server=server.rstrip("/"), ssl_context=ssl_ctx, static_headers=headers,
                         header_provider=provider, namespace=ctx.get("namespace"),
-                        source=":".join(paths), context_name=ctx_name)
+                        source=":".join(paths), context_name=ctx_name,
+                        tls_server_name=cluster.get("tls-server-name") or None)
 
 
 def load_incluster_config(sa_dir: str = SA_DIR, environ: Optional[Dict[str, str]] = None,

@@ -432,7 +432,7 @@ class HttpClient:
     def __init__(self, base_url: str, ssl_context: Optional[_ssl.SSLContext] = None,
                  headers: Optional[Dict[str, str]] = None, timeout: float = 30.0,
                  header_provider: Optional[Callable[[], Dict[str, str]]] = None,
-                 max_idle: int = 8) -> None:
+                 max_idle: int = 8, server_name: Optional[str] = None) -> None:
         u = urlsplit(base_url)
         if u.scheme not in ("http", "https"):
             raise ValueError(f"unsupported URL scheme in {base_url!r}")
@@ -447,6 +447,8 @@ class HttpClient:
         if u.scheme == "https" and ssl_context is None:
             ssl_context = _ssl.create_default_context()
         self.ssl_context = ssl_context if u.scheme == "https" else None
+        # SNI and certificate host name (kubeconfig ``tls-server-name``); the URL host otherwise
+        self.server_name = server_name or self.host
         self.headers = dict(headers or {})
         self.header_provider = header_provider
         self.timeout = timeout
@@ -478,7 +480,7 @@ class HttpClient:
             _, proto = await with_timeout(
                 loop.create_connection(lambda: _ClientProtocol(loop), self.host, self.port,
                                        ssl=self.ssl_context,
-                                       server_hostname=self.host if self.ssl_context else None),
+                                       server_hostname=self.server_name if self.ssl_context else None),
                 timeout)
         except asyncio.TimeoutError:
             raise HttpError(f"connect to {self.host}:{self.port} timed out") from None

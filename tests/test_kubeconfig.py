@@ -119,6 +119,21 @@ def test_exec_credential_plugin(tmp_path):
     assert load_kube_config(p).auth_headers() == {"Authorization": "Bearer exec-42"}
 
 
+def test_exec_credential_relative_command(tmp_path):
+    # client-go: a command with a path separator resolves against the kubeconfig's directory
+    (tmp_path / "bin").mkdir()
+    plugin = tmp_path / "bin" / "cred.sh"
+    plugin.write_text('#!/bin/sh\necho \'{"kind":"ExecCredential","status":{"token":"rel-tok"}}\'\n')
+    plugin.chmod(0o755)
+    p = write(tmp_path / "cfg", """
+        current-context: x
+        clusters: [{name: c, cluster: {server: "http://h"}}]
+        contexts: [{name: x, context: {cluster: c, user: u}}]
+        users: [{name: u, user: {exec: {command: ./bin/cred.sh, env: [{name: ONLY_NAME}]}}}]
+        """)
+    assert load_kube_config(p).auth_headers() == {"Authorization": "Bearer rel-tok"}
+
+
 def test_repo_dummy_kubeconfig():
     """assets/config (C13): plain HTTP to localhost:9988 with a bearer token."""
     ep = load_kube_config(os.path.join(ROOT, "assets", "config"))
@@ -173,3 +188,36 @@ def test_tls_with_ca_data_and_client_cert(tmp_path):
         return ver
 
     assert run(body())["gitVersion"].startswith("v1.33")
+
+
+def test_tls_server_name_is_verified(tmp_path):
+    # tls-server-name: SNI and the certificate check use that name, not the
+    # URL host (the server certificate covers "localhost", not "wrong.example")
+    from k8s_watcher_amd.net.http import HttpError
+
+    pki = make_pki(str(tmp_path / "pki"))
+    server_ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+    server_ctx.load_cert_chain(pki.server_crt, pki.server_key)
+
+    async def body(name):
+        srv = FakeApiServer()
+        await srv.start(ssl_context=server_ctx)
+        cfg = write(tmp_path / f"cfg-{name}", f"""
+            current-context: x
+            clusters: [{{name: c, cluster: {{server: "https://127.0.0.1:{srv.port}",
+                                           certificate-authority: {pki.ca_crt}, tls-server-name: {name}}}}}]
+            contexts: [{{name: x, context: {{cluster: c, user: u}}}}]
+            users: [{{name: u, user: {{}}}}]
+            """)
+        ep = load_kube_config(cfg)
+        assert ep.tls_server_name == name
+        api = KubeApi(ep)
+        try:
+            return await api.get_version()
+        finally:
+            await api.close()
+            await srv.stop()
+
+    assert run(body("localhost"))["gitVersion"].startswith("v1.33")
+    with pytest.raises(HttpError, match="CERTIFICATE_VERIFY_FAILED|match"):
+        run(body("wrong.example"))
