@@ -13,7 +13,8 @@ Format, one JSON object per line::
     {"t": 0.0,   "type": "LIST",     "object": {...pod...}}    # state at start
     {"t": 1.234, "type": "MODIFIED", "object": {...pod...}}    # watch events, t = seconds since start
 
-``BOOKMARK`` and ``ERROR`` events are not recorded (a replay makes its own).
+``BOOKMARK`` and ``ERROR`` events are not recorded (a replay makes its own); bookmarks
+only advance the resume point, an ``ERROR`` (e.g. 410) ends the capture.
 
     python -m k8s_watcher_amd.tools.capture production --out pods.ndjson --seconds 600
     python -m k8s_watcher_amd.tools.capture --kubeconfig ~/.kube/config --namespace default --max-events 10000
@@ -48,36 +49,62 @@ async def capture(api: KubeApi, out, namespace: Optional[str] = None, seconds: f
     n = 0
     buf = bytearray()
     done = asyncio.Event()
+    expired: List[str] = []
 
     def sink(data, _read_ns: int) -> None:
-        nonlocal n
+        nonlocal n, rv
         buf.extend(data)
-        *lines, rest = bytes(buf).split(b"\n")
-        buf[:] = rest
+        cut = buf.rfind(b"\n")
+        if cut < 0:
+            return
+        lines = bytes(buf[:cut]).split(b"\n")
+        del buf[:cut + 1]
         now = round(time.monotonic() - t0, 6)
         for line in lines:
-            if not line.strip():
+            if not line.strip() or done.is_set():
                 continue
             ev = json.loads(line)
-            if ev.get("type") not in ("ADDED", "MODIFIED", "DELETED"):
+            obj = ev.get("object") or {}
+            etype = ev.get("type")
+            if etype == "ERROR":
+                expired.append(str(obj.get("message") or obj))
+                done.set()
                 continue
-            out.write(json.dumps({"t": now, "type": ev["type"], "object": ev["object"]},
-                                 separators=(",", ":")) + "\n")
+            rv = (obj.get("metadata") or {}).get("resourceVersion") or rv
+            if etype not in ("ADDED", "MODIFIED", "DELETED"):
+                continue
+            out.write(json.dumps({"t": now, "type": etype, "object": obj}, separators=(",", ":")) + "\n")
             n += 1
             if max_events and n >= max_events:
                 done.set()
 
-    stream = await api.watch_pods(sink, namespace=namespace, resource_version=rv, allow_bookmarks=False)
-    waiters = [stream.finished, asyncio.ensure_future(done.wait())]
+    deadline = t0 + seconds if seconds else None
+    waiters = [asyncio.ensure_future(done.wait())]
     if stop is not None:
         waiters.append(asyncio.ensure_future(stop.wait()))
     try:
-        # until --seconds, --max-events, a stop request, or the server ending the watch
-        await asyncio.wait(waiters, timeout=seconds or None, return_when=asyncio.FIRST_COMPLETED)
+        # until --seconds, --max-events, a stop request or an ERROR event; a
+        # watch the server ends (its request timeout) resumes from the last
+        # resourceVersion, so a long capture is not cut short
+        while not any(w.done() for w in waiters):
+            left = None if deadline is None else deadline - time.monotonic()
+            if left is not None and left <= 0:
+                break
+            buf.clear()
+            opened = time.monotonic()
+            stream = await api.watch_pods(sink, namespace=namespace, resource_version=rv, allow_bookmarks=True)
+            try:
+                await asyncio.wait([stream.finished] + waiters, timeout=left,
+                                   return_when=asyncio.FIRST_COMPLETED)
+            finally:
+                stream.close()
+            if time.monotonic() - opened < 1.0 and not any(w.done() for w in waiters):
+                await asyncio.wait(waiters, timeout=1.0)  # pace a server that hangs up at once
     finally:
-        for w in waiters[1:]:
+        for w in waiters:
             w.cancel()
-        stream.close()
+    if expired:
+        print(f"watch ended with an ERROR event: {expired[0]}", file=sys.stderr)
     out.flush()
     return n
 

@@ -2,6 +2,7 @@
 
 import asyncio
 import io
+import json
 
 from conftest import run
 from k8s_watcher_amd.kube.api import KubeApi
@@ -57,4 +58,28 @@ def test_capture_then_replay_gives_the_same_notifications(tmp_path):
         await svc.shutdown()
         await sink.stop()
         await srv.stop()
+    run(body())
+
+
+def test_capture_resumes_when_the_server_ends_the_watch(tmp_path):
+    async def body():
+        src = FakeApiServer()
+        f = PodFactory(seed=53, namespaces=["default"])
+        await src.start()
+        api = KubeApi(KubeEndpoint(server=src.url))
+        out = io.StringIO()
+        task = asyncio.ensure_future(capture(api, out, max_events=6))
+        await asyncio.sleep(0.2)
+        pods = [src.create(f.running(f.new_pod())) for _ in range(3)]
+        await asyncio.sleep(0.2)
+        src.drop_connections()  # API server restart: the capture re-watches from the last RV
+        await asyncio.sleep(1.2)
+        for p in pods:
+            src.update(f.terminated(p))
+        n = await asyncio.wait_for(task, 10)
+        await api.close()
+        await src.stop()
+        recs = [json.loads(line) for line in out.getvalue().splitlines()]
+        assert n == 6
+        assert [r["type"] for r in recs] == ["ADDED"] * 3 + ["MODIFIED"] * 3  # nothing lost, nothing twice
     run(body())
