@@ -28,6 +28,7 @@ import os
 import ssl
 import subprocess
 import tempfile
+import threading
 import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Tuple
@@ -185,12 +186,25 @@ class _ExecCredential:
         self.base = base  # a relative command path resolves against the kubeconfig's directory
         self._token: Optional[str] = None
         self._expiry: float = 0.0
+        self._bg: Optional[threading.Thread] = None
 
     def headers(self) -> Dict[str, str]:
         now = time.time()
         if self._token is None or (self._expiry and now >= self._expiry - 10):
-            self._refresh()
+            self._refresh()  # no usable token: the request has to wait for the plugin
+        elif self._expiry and now >= self._expiry - 120 and self._bg is None:
+            # still valid: refresh on a thread so the event loop does not block on the plugin
+            self._bg = threading.Thread(target=self._refresh_bg, daemon=True)
+            self._bg.start()
         return {"Authorization": f"Bearer {self._token}"} if self._token else {}
+
+    def _refresh_bg(self) -> None:
+        try:
+            self._refresh()
+        except ConfigException:
+            pass  # retried in the foreground once the current token expires
+        finally:
+            self._bg = None
 
     def _refresh(self) -> None:
         cmd = [self.spec.get("command")] + list(self.spec.get("args") or [])

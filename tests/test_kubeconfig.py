@@ -221,3 +221,34 @@ def test_tls_server_name_is_verified(tmp_path):
     assert run(body("localhost"))["gitVersion"].startswith("v1.33")
     with pytest.raises(HttpError, match="CERTIFICATE_VERIFY_FAILED|match"):
         run(body("wrong.example"))
+
+
+def test_exec_credential_refreshes_in_background_before_expiry(tmp_path):
+    import time
+
+    from k8s_watcher_amd.kube.kubeconfig import _ExecCredential
+
+    counter = tmp_path / "n"
+    plugin = tmp_path / "plugin.py"
+    plugin.write_text(textwrap.dedent(f"""
+        import datetime, json
+        p = {str(counter)!r}
+        try:
+            n = int(open(p).read())
+        except OSError:
+            n = 0
+        open(p, "w").write(str(n + 1))
+        exp = datetime.datetime.now(datetime.timezone.utc) + datetime.timedelta(seconds=60)
+        print(json.dumps({{"kind": "ExecCredential", "status": {{"token": "t%d" % n,
+              "expirationTimestamp": exp.strftime("%Y-%m-%dT%H:%M:%SZ")}}}}))
+        """))
+    cred = _ExecCredential({"command": sys.executable, "args": [str(plugin)]})
+    assert cred.headers() == {"Authorization": "Bearer t0"}  # first token: fetched in the foreground
+    # 60 s left (< 120 s): the next call answers at once with the current token
+    # and refreshes on a thread
+    assert cred.headers() == {"Authorization": "Bearer t0"}
+    deadline = time.time() + 20
+    while cred._bg is not None and time.time() < deadline:
+        time.sleep(0.05)
+    assert cred.headers()["Authorization"] in ("Bearer t1", "Bearer t2")
+    assert int(counter.read_text()) >= 2
