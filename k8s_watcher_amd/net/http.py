@@ -23,6 +23,7 @@ import zlib
 from typing import Callable, Dict, List, Optional, Tuple
 from urllib.parse import urlencode, urlsplit
 from ..utils.aio import with_timeout
+from .sockopt import DEFAULT_KEEPALIVE_SECONDS, tune_socket
 
 
 class HttpError(Exception):
@@ -432,7 +433,8 @@ class HttpClient:
     def __init__(self, base_url: str, ssl_context: Optional[_ssl.SSLContext] = None,
                  headers: Optional[Dict[str, str]] = None, timeout: float = 30.0,
                  header_provider: Optional[Callable[[], Dict[str, str]]] = None,
-                 max_idle: int = 8, server_name: Optional[str] = None) -> None:
+                 max_idle: int = 8, server_name: Optional[str] = None,
+                 keepalive: float = DEFAULT_KEEPALIVE_SECONDS) -> None:
         u = urlsplit(base_url)
         if u.scheme not in ("http", "https"):
             raise ValueError(f"unsupported URL scheme in {base_url!r}")
@@ -453,6 +455,7 @@ class HttpClient:
         self.header_provider = header_provider
         self.timeout = timeout
         self.max_idle = max_idle
+        self.keepalive = keepalive  # TCP keep-alive / user timeout, seconds (net/sockopt.py)
         self._idle: List[_ClientProtocol] = []
         self._all: List[_ClientProtocol] = []
 
@@ -477,7 +480,7 @@ class HttpClient:
     async def _connect(self, timeout: float) -> _ClientProtocol:
         loop = asyncio.get_running_loop()
         try:
-            _, proto = await with_timeout(
+            transport, proto = await with_timeout(
                 loop.create_connection(lambda: _ClientProtocol(loop), self.host, self.port,
                                        ssl=self.ssl_context,
                                        server_hostname=self.server_name if self.ssl_context else None),
@@ -486,6 +489,7 @@ class HttpClient:
             raise HttpError(f"connect to {self.host}:{self.port} timed out") from None
         except OSError as exc:
             raise HttpError(f"connect to {self.host}:{self.port} failed: {exc}") from None
+        tune_socket(transport.get_extra_info("socket"), self.keepalive)
         self._all.append(proto)
         return proto
 

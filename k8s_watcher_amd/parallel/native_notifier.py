@@ -33,6 +33,7 @@ from urllib.parse import urlsplit
 
 from ..metrics import _BUCKETS_NS, Metrics
 from ..net.http import HttpClient
+from ..net.sockopt import tune_socket
 from ..ops.native import load
 from ..utils.aio import with_timeout
 from ..utils.backoff import Backoff
@@ -219,7 +220,7 @@ class NativeNotifierPool:
             family, stype, proto, _, sa = await self._resolve()
             sock = socket.socket(family, stype, proto)
             sock.setblocking(False)
-            sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            tune_socket(sock)
             await with_timeout(self.loop.sock_connect(sock, sa), self.settings.timeout)
         except (OSError, asyncio.TimeoutError) as exc:
             if sock is not None:

@@ -41,6 +41,7 @@ from urllib.parse import urlsplit
 from ..metrics import Metrics
 from ..models.payload import finish_body
 from ..net.http import response_scanner
+from ..net.sockopt import tune_socket
 from ..utils.backoff import Backoff
 from ..utils.config import ClusterApiSettings, RetryPolicy
 from ..utils.fastlog import EventLog
@@ -85,6 +86,7 @@ class _Conn(asyncio.Protocol):
     # ------------------------------------------------------------- asyncio protocol
     def connection_made(self, transport) -> None:  # type: ignore[override]
         self.transport = transport
+        tune_socket(transport.get_extra_info("socket"))
         self.state = self.UP
         self.connect_backoff.reset()
         self.scanner.reset()
