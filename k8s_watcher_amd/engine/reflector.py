@@ -22,7 +22,9 @@ This reflector:
   API servers without it;
 * on transport errors backs off per ``watcher.retry`` and gives up after
   ``max_attempts`` consecutive failures (0 = never), raising
-  :class:`WatchFailed`;
+  :class:`WatchFailed`; waits at least the server's ``Retry-After``, and a
+  ``429`` (API Priority and Fairness throttling) is waited out without
+  counting toward ``max_attempts``;
 * pauses its socket while the notifier reports backpressure.
 """
 
@@ -355,6 +357,13 @@ class Reflector:
                     self.log.warning(f"Watch resourceVersion {self.rv} expired (410); relisting")
                     need_list = True
                     continue
+                if exc.status == 429:
+                    # throttled by API Priority and Fairness: wait as asked but
+                    # do not count it toward max_attempts — exiting and
+                    # relisting would only add load to a busy API server
+                    self.metrics.c["api_throttled"] += 1
+                    await self._backoff(backoff, 0, exc)
+                    continue
                 failures += 1
                 await self._backoff(backoff, failures, exc)
             except HttpError as exc:
@@ -365,11 +374,20 @@ class Reflector:
 
     async def _backoff(self, backoff: Backoff, failures: int, exc: Exception) -> None:
         limit = self.settings.watcher.retry.max_attempts
-        if limit and failures >= limit:
+        if limit and failures and failures >= limit:
             self.log.error(f"Error in Pod watcher: {exc}")
             raise WatchFailed(str(exc)) from exc
         delay = backoff.next_delay()
-        self.log.warning(f"Watch failed ({exc}); retry {failures}/{limit or 'inf'} in {delay:.2f}s")
+        retry_after = getattr(exc, "retry_after", None)
+        if retry_after is not None:
+            # the API server named its own wait (429 under API Priority and
+            # Fairness, 503 while starting): honour it, never retry sooner
+            delay = max(delay, retry_after)
+            self.metrics.c["retry_after_waits"] += 1
+        if failures:
+            self.log.warning(f"Watch failed ({exc}); retry {failures}/{limit or 'inf'} in {delay:.2f}s")
+        else:
+            self.log.warning(f"Watch throttled ({exc}); retry in {delay:.2f}s")
         self.metrics.c["watch_restarts"] += 1
         await self._sleep(delay)
 

@@ -22,10 +22,14 @@ USER_AGENT = "k8s-watcher-amd/1.0"
 class ApiError(Exception):
     """Non-2xx answer from the API server (``status`` = HTTP code)."""
 
-    def __init__(self, status: int, reason: str, body: bytes) -> None:
+    def __init__(self, status: int, reason: str, body: bytes,
+                 headers: Optional[Dict[str, str]] = None) -> None:
         self.status = status
         self.reason = reason
         self.body = body
+        # seconds the server asked us to wait (429 from API Priority and
+        # Fairness, 503 while starting); None when absent or not delta-seconds
+        self.retry_after = parse_retry_after((headers or {}).get("retry-after"))
         msg = reason
         try:
             doc = json.loads(body)
@@ -34,6 +38,19 @@ class ApiError(Exception):
         except (ValueError, AttributeError):
             self.k8s_reason = None
         super().__init__(f"({status}) {msg}")
+
+
+def parse_retry_after(value: Optional[str], cap: float = 300.0) -> Optional[float]:
+    """``Retry-After: <delta-seconds>`` → float, capped at ``cap`` (HTTP-dates are ignored)."""
+    if not value:
+        return None
+    try:
+        secs = float(value.strip())
+    except ValueError:
+        return None
+    if secs != secs or secs < 0:
+        return None
+    return min(secs, cap)
 
 
 def pods_path(namespace: Optional[str] = None) -> str:
@@ -56,7 +73,7 @@ class KubeApi:
                    timeout: Optional[float] = None, headers: Optional[Dict[str, str]] = None) -> Response:
         resp = await self.http.request("GET", path, query=query, timeout=timeout, headers=headers)
         if not resp.ok:
-            raise ApiError(resp.status, resp.reason, resp.body)
+            raise ApiError(resp.status, resp.reason, resp.body, resp.headers)
         return resp
 
     async def get_version(self) -> Dict[str, object]:
@@ -123,7 +140,7 @@ class KubeApi:
                                              timeout=connect_timeout, raw_chunked=raw_chunked,
                                              on_mode=on_mode, read_size=read_size, zero_copy=zero_copy)
         if err is not None:
-            raise ApiError(stream.status, stream.reason, err)
+            raise ApiError(stream.status, stream.reason, err, stream.headers)
         return stream
 
     # ------------------------------------------------------------------ coordination.k8s.io/v1
@@ -135,7 +152,7 @@ class KubeApi:
         hdrs = None if body is None else {"Content-Type": "application/json"}
         resp = await self.http.request(method, path, headers=hdrs, body=body, timeout=timeout)
         if not resp.ok:
-            raise ApiError(resp.status, resp.reason, resp.body)
+            raise ApiError(resp.status, resp.reason, resp.body, resp.headers)
         return resp.json() if resp.body else {}
 
     async def get_lease(self, namespace: str, name: str, timeout: Optional[float] = None) -> Optional[Dict]:

@@ -40,6 +40,8 @@ COUNTERS = (
     "spool_dropped",
     "watch_restarts",
     "short_watches",        # watches the server ended at once with nothing in them (backed off)
+    "api_throttled",        # 429 answers from the API server (not counted against watcher.retry)
+    "retry_after_waits",    # retries delayed to the API server's Retry-After
     "relists",
     "watch_list_syncs",     # initial state via WatchList (sendInitialEvents) instead of LIST
     "expired_410",

@@ -148,7 +148,7 @@ class FakeApiServer:
         self.compacted_rv = start_rv
         self.watches: Set[_Watch] = set()
         self.writers: Set[asyncio.StreamWriter] = set()
-        self.fail_next: List[Tuple[int, str]] = []
+        self.fail_next: List[Tuple[int, str, Optional[float]]] = []
         self.empty_watches = 0
         self.requests: List[Tuple[str, str]] = []
         self.server: Optional[asyncio.AbstractServer] = None
@@ -301,9 +301,12 @@ class FakeApiServer:
                 pass
         self.writers.clear()
 
-    def fail_requests(self, n: int, status: int = 500, path_prefix: str = "") -> None:
+    def fail_requests(self, n: int, status: int = 500, path_prefix: str = "",
+                      retry_after: Optional[float] = None) -> None:
+        """Answer the next ``n`` requests under ``path_prefix`` with ``status``
+        (and a ``Retry-After`` header when given, as APF's 429 carries)."""
         for _ in range(n):
-            self.fail_next.append((status, path_prefix))
+            self.fail_next.append((status, path_prefix, retry_after))
 
     def hang_up_watches(self, n: int) -> None:
         """The next ``n`` watches get a 200 with an empty body that ends at once
@@ -347,12 +350,13 @@ class FakeApiServer:
             except Exception:  # noqa: BLE001
                 pass
 
-    def _send_json(self, writer, code: int, doc: Any, reason: str = "OK", gzip_ok: bool = False) -> None:
+    def _send_json(self, writer, code: int, doc: Any, reason: str = "OK", gzip_ok: bool = False,
+                   extra_headers: Optional[Dict[str, str]] = None) -> None:
         body = json.dumps(doc, separators=(",", ":"), ensure_ascii=False).encode("utf-8")
-        extra = b""
+        extra = b"".join(f"{k}: {v}\r\n".encode("latin-1") for k, v in (extra_headers or {}).items())
         if gzip_ok and len(body) > GZIP_THRESHOLD:  # as the API server: only large responses
             body = gzip.compress(body, compresslevel=1)
-            extra = b"Content-Encoding: gzip\r\n"
+            extra += b"Content-Encoding: gzip\r\n"
             self.gzipped_responses += 1
         writer.write(b"HTTP/1.1 %d %s\r\nContent-Type: application/json\r\n%sContent-Length: %d\r\n\r\n"
                      % (code, reason.encode(), extra, len(body)) + body)
@@ -366,10 +370,13 @@ class FakeApiServer:
             self._send_json(writer, 401, _status(401, "Unauthorized", "Unauthorized"), "Unauthorized")
             return True
         if self.fail_next:
-            st, prefix = self.fail_next[0]
+            st, prefix, retry_after = self.fail_next[0]
             if path.startswith(prefix):
                 self.fail_next.pop(0)
-                self._send_json(writer, st, _status(st, "InternalError", "injected failure"), "Injected")
+                reason = "TooManyRequests" if st == 429 else "InternalError"
+                self._send_json(writer, st, _status(st, reason, "injected failure"), "Injected",
+                                extra_headers=None if retry_after is None
+                                else {"Retry-After": f"{retry_after:g}"})
                 return True
         if path == "/apis/authorization.k8s.io/v1/selfsubjectaccessreviews" and method == "POST":
             try:

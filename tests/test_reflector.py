@@ -183,6 +183,53 @@ def test_retry_budget_exhausted_is_fatal():
     run(body())
 
 
+def test_parse_retry_after():
+    from k8s_watcher_amd.kube.api import parse_retry_after
+    assert parse_retry_after("1") == 1.0
+    assert parse_retry_after(" 2.5 ") == 2.5
+    assert parse_retry_after("9999") == 300.0  # capped
+    for bad in (None, "", "-1", "nan", "Wed, 21 Oct 2015 07:28:00 GMT"):
+        assert parse_retry_after(bad) is None
+
+
+def test_429_honours_retry_after_without_spending_retry_budget():
+    # API Priority and Fairness answers 429 + Retry-After: the watcher waits
+    # as asked and does not exit after max_attempts throttled requests
+    async def body():
+        async with Stack() as st:
+            svc = st.service({"watcher": {"retry": {"delay_seconds": 0.01, "max_attempts": 2}}})
+            await svc.start()
+            st.srv.fail_requests(4, 429, "/api/v1/pods", retry_after=0.15)
+            t0 = time.monotonic()
+            st.srv.drop_connections()
+            evs = lifecycle_apply(st, 2)
+            await st.settle(len(evs))
+            assert_exactly_once(st.delivered(), evs)
+            assert time.monotonic() - t0 >= 4 * 0.15 * 0.9  # waited Retry-After, not the 10 ms backoff
+            assert svc.metrics.c["api_throttled"] == 4
+            assert svc.metrics.c["retry_after_waits"] == 4
+            assert not any(t.done() for t in svc._tasks)
+
+    run(body())
+
+
+def test_retry_after_on_5xx_counts_as_failure_but_waits():
+    async def body():
+        async with Stack() as st:
+            svc = st.service({"watcher": {"retry": {"delay_seconds": 0.01, "max_attempts": 5}}})
+            await svc.start()
+            st.srv.fail_requests(2, 503, "/api/v1/pods", retry_after=0.2)
+            t0 = time.monotonic()
+            st.srv.drop_connections()
+            evs = lifecycle_apply(st, 1)
+            await st.settle(len(evs))
+            assert time.monotonic() - t0 >= 2 * 0.2 * 0.9
+            assert svc.metrics.c["retry_after_waits"] == 2
+            assert svc.metrics.c["api_throttled"] == 0
+
+    run(body())
+
+
 def test_short_watches_back_off_without_failing():
     # a proxy that ends every watch at once: reconnects are paced by the
     # backoff (no hot loop) and do not spend the failure budget
