@@ -13,7 +13,7 @@ from __future__ import annotations
 import json
 from typing import Callable, Dict, Optional, Tuple
 
-from ..net.http import HttpClient, HttpError, Response, StreamResponse
+from ..net.http import HttpClient, HttpError, Response, StreamResponse, parse_retry_after  # noqa: F401
 from .kubeconfig import KubeEndpoint
 
 USER_AGENT = "k8s-watcher-amd/1.0"
@@ -38,19 +38,6 @@ class ApiError(Exception):
         except (ValueError, AttributeError):
             self.k8s_reason = None
         super().__init__(f"({status}) {msg}")
-
-
-def parse_retry_after(value: Optional[str], cap: float = 300.0) -> Optional[float]:
-    """``Retry-After: <delta-seconds>`` → float, capped at ``cap`` (HTTP-dates are ignored)."""
-    if not value:
-        return None
-    try:
-        secs = float(value.strip())
-    except ValueError:
-        return None
-    if secs != secs or secs < 0:
-        return None
-    return min(secs, cap)
 
 
 def pods_path(namespace: Optional[str] = None) -> str:

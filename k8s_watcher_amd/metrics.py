@@ -32,6 +32,7 @@ COUNTERS = (
     "notify_delivered",
     "notify_failed",
     "notify_retried",
+    "notify_retry_after_waits",  # retries delayed to clusterapi's Retry-After
     "notify_superseded",
     "notify_coalesced",
     "notify_spooled",       # owed notifications written to the spool (parallel/spool.py)

@@ -250,11 +250,25 @@ class ResponseParser:
             raise HttpError("connection closed mid-response")
 
 
+def parse_retry_after(value: Optional[str], cap: float = 300.0) -> Optional[float]:
+    """``Retry-After: <delta-seconds>`` → float, capped at ``cap`` (HTTP-dates are ignored)."""
+    if not value:
+        return None
+    try:
+        secs = float(value.strip())
+    except ValueError:
+        return None
+    if secs != secs or secs < 0:
+        return None
+    return min(secs, cap)
+
+
 class PyResponseScanner:
     """Python twin of ``_kwcore.ResponseScanner`` (same results, used without the extension).
 
     ``feed(data)`` returns one item per complete response: the int status for
-    a 2xx keep-alive response, else ``(status, keep_alive, body)``.
+    a 2xx keep-alive response, else ``(status, keep_alive, body, retry_after)``
+    with ``retry_after`` in seconds, ``-1.0`` without a ``Retry-After`` header.
     """
 
     def __init__(self) -> None:
@@ -270,7 +284,7 @@ class PyResponseScanner:
         if 200 <= p.status < 300 and p.keep_alive:
             self._done.append(p.status)
         else:
-            self._done.append((p.status, p.keep_alive, p.body()))
+            self._done.append((p.status, p.keep_alive, p.body(), _retry_after(p)))
 
     def reset(self) -> None:
         self._done = []
@@ -286,10 +300,15 @@ class PyResponseScanner:
             raise ValueError(str(exc)) from None
         if self.parser.state == ResponseParser.UNTIL_CLOSE and self.parser.body_parts:
             p = self.parser
-            self._done.append((p.status, False, p.body()))
+            self._done.append((p.status, False, p.body(), _retry_after(p)))
             self._arm()
         out, self._done = self._done, []
         return out
+
+
+def _retry_after(p: "ResponseParser") -> float:
+    ra = parse_retry_after(p.headers.get("retry-after"))
+    return -1.0 if ra is None else ra
 
 
 def response_scanner(native: bool = True):

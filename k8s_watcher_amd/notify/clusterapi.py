@@ -22,7 +22,7 @@ import logging
 import time
 from typing import Any, Dict, Optional
 
-from ..net.http import HttpClient, HttpError
+from ..net.http import HttpClient, HttpError, parse_retry_after
 from ..utils.config import RetryPolicy
 from ..utils.logsetup import NOTIFIER_LOGGER
 
@@ -78,9 +78,11 @@ class ClusterApiClient(_Common):
         body = json.dumps(pod_data).encode("utf-8")
         for attempt in range(1, max(1, self.retry.max_attempts) + 1):
             status = None
+            retry_after = None
             try:
                 resp = self.session.post(ep, data=body, timeout=self.timeout, **self._tls_kw)
                 status = resp.status_code
+                retry_after = parse_retry_after(resp.headers.get("Retry-After"))
                 if 200 <= status < 300:
                     self.logger.info(f"Successfully updated pod data for {pod_data.get('name', 'unknown')}")
                     return True
@@ -95,7 +97,7 @@ class ClusterApiClient(_Common):
             if status is not None and status not in RETRYABLE:
                 return False
             if attempt < self.retry.max_attempts:
-                time.sleep(self.retry.delay(attempt))
+                time.sleep(max(self.retry.delay(attempt), retry_after or 0.0))
         return False
 
     def health_check(self) -> bool:
@@ -127,9 +129,11 @@ class AsyncClusterApiClient(_Common):
         body = json.dumps(pod_data).encode("utf-8")
         for attempt in range(1, max(1, self.retry.max_attempts) + 1):
             status = None
+            retry_after = None
             try:
                 resp = await self.http.request("POST", self.pod_update, body=body)
                 status = resp.status
+                retry_after = parse_retry_after(resp.headers.get("retry-after"))
                 if resp.ok:
                     return True
                 self.logger.error(f"Failed to update pod data. Status: {status}, Response: {resp.text()}")
@@ -138,7 +142,7 @@ class AsyncClusterApiClient(_Common):
             if status is not None and status not in RETRYABLE:
                 return False
             if attempt < self.retry.max_attempts:
-                await asyncio.sleep(self.retry.delay(attempt))
+                await asyncio.sleep(max(self.retry.delay(attempt), retry_after or 0.0))
         return False
 
     async def health_check(self) -> bool:

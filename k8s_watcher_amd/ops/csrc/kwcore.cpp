@@ -1561,10 +1561,27 @@ bool contains_token_ci(const char* p, const char* e, const char* tok) {
     return false;
 }
 
+// Retry-After: <delta-seconds> (fractions accepted, capped at 300 s); -1 when
+// absent or an HTTP-date (which clusterapi-style services do not send).
+double parse_retry_after(const char* v, const char* e) {
+    while (v < e && (*v == ' ' || *v == '\t')) ++v;
+    if (v >= e || !is_digit(*v)) return -1.0;
+    double secs = 0.0;
+    while (v < e && is_digit(*v)) secs = secs * 10.0 + (*v++ - '0');
+    if (v < e && *v == '.') {
+        double scale = 0.1;
+        for (++v; v < e && is_digit(*v); ++v, scale *= 0.1) secs += (*v - '0') * scale;
+    }
+    while (v < e && (*v == ' ' || *v == '\t')) ++v;
+    if (v != e) return -1.0;
+    return secs > 300.0 ? 300.0 : secs;
+}
+
 // Try to parse one complete response at b[0..n). Returns bytes consumed (0 =
-// incomplete, SIZE_MAX = malformed); fills status, keep_alive, body span.
+// incomplete, SIZE_MAX = malformed); fills status, keep_alive, body span and
+// retry_after (seconds, -1 = no Retry-After header).
 size_t scan_response(const char* b, size_t n, int& status, bool& keep_alive, std::string& body,
-                     bool& until_close) {
+                     bool& until_close, double& retry_after) {
     const char* e = b + n;
     const char* he = nullptr;
     for (const char* q = b; q + 3 < e; ++q) {
@@ -1586,6 +1603,7 @@ size_t scan_response(const char* b, size_t n, int& status, bool& keep_alive, std
         status = status * 10 + (sp[i] - '0');
     }
     long long clen = -1;
+    retry_after = -1.0;
     bool chunked = false, conn_close = false, conn_keep = false;
     const char* line = (const char*)std::memchr(b, '\n', (size_t)(he - b));
     while (line && line < he) {
@@ -1602,6 +1620,8 @@ size_t scan_response(const char* b, size_t n, int& status, bool& keep_alive, std
         } else if (ieq_prefix(ls, le, "connection:")) {
             conn_close = contains_token_ci(ls + 11, le, "close");
             conn_keep = contains_token_ci(ls + 11, le, "keep-alive");
+        } else if (ieq_prefix(ls, le, "retry-after:")) {
+            retry_after = parse_retry_after(ls + 12, le);
         }
         line = (const char*)std::memchr(ls, '\n', (size_t)(he + 2 - ls));
         if (line && line >= he) break;
@@ -1689,7 +1709,8 @@ PyObject* Scanner_feed(ScannerObject* self, PyObject* arg) {
     while (ok && pos < n) {
         int status = 0;
         bool keep = true, until_close = false;
-        size_t used = scan_response(data + pos, n - pos, status, keep, body, until_close);
+        double retry_after = -1.0;
+        size_t used = scan_response(data + pos, n - pos, status, keep, body, until_close, retry_after);
         if (used == 0) break;
         if (used == SIZE_MAX) {
             PyErr_SetString(PyExc_ValueError, "malformed HTTP response");
@@ -1701,8 +1722,8 @@ PyObject* Scanner_feed(ScannerObject* self, PyObject* arg) {
         if (status >= 200 && status < 300 && keep) {
             item = PyLong_FromLong(status);
         } else {
-            item = Py_BuildValue("(iOy#)", status, keep ? Py_True : Py_False, body.data(),
-                                 (Py_ssize_t)body.size());
+            item = Py_BuildValue("(iOy#d)", status, keep ? Py_True : Py_False, body.data(),
+                                 (Py_ssize_t)body.size(), retry_after);
         }
         if (!item || PyList_Append(out, item) < 0) ok = false;
         Py_XDECREF(item);

@@ -110,11 +110,11 @@ class _Conn(asyncio.Protocol):
                 if r.__class__ is int:
                     pool._delivered(req)
                     continue
-                status, keep_alive, body = r
+                status, keep_alive, body, retry_after = r
                 if 200 <= status < 300:
                     pool._delivered(req)
                 else:
-                    pool._failed(req, status, body[:500].decode("utf-8", "replace"))
+                    pool._failed(req, status, body[:500].decode("utf-8", "replace"), retry_after)
                 if not keep_alive and self.transport is not None:
                     self.transport.close()
                     pool.elog.flush()
@@ -469,7 +469,8 @@ class NotifierPool:
                           f"Successfully notified clusterapi about {req.etype} event for {req.ns}/{req.name}")
         self._finish(req)
 
-    def _failed(self, req: NotifyRequest, status: Optional[int], detail: str) -> None:
+    def _failed(self, req: NotifyRequest, status: Optional[int], detail: str,
+                retry_after: float = -1.0) -> None:
         if status is not None:
             self.log.error(f"Failed to update pod data. Status: {status}, Response: {detail}")
         else:
@@ -482,6 +483,9 @@ class NotifierPool:
         if retryable and req.attempts < self.retry_policy.max_attempts and not self.closing:
             self.metrics.c["notify_retried"] += 1
             delay = self.retry_policy.delay(req.attempts)
+            if retry_after > delay:  # clusterapi named its own wait (429/503): never retry sooner
+                delay = retry_after
+                self.metrics.c["notify_retry_after_waits"] += 1
             self.retrying[req.seq] = req
             self.loop.call_later(delay, self._retry_fire, req)
             return

@@ -29,14 +29,15 @@ from ..utils.aio import with_timeout
 _OK = b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nContent-Length: 15\r\n\r\n{\"status\":\"ok\"}"
 
 
-def _resp(status: int, body: bytes = b"{}") -> bytes:
+def _resp(status: int, body: bytes = b"{}", retry_after: Optional[float] = None) -> bytes:
     reason = {200: "OK", 201: "Created", 204: "No Content", 400: "Bad Request", 404: "Not Found",
               429: "Too Many Requests", 500: "Internal Server Error",
               503: "Service Unavailable"}.get(status, "Status")
     if status == 204:
         return b"HTTP/1.1 204 No Content\r\n\r\n"
-    return b"HTTP/1.1 %d %s\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n%s" % (
-        status, reason.encode(), len(body), body)
+    extra = b"" if retry_after is None else b"Retry-After: %s\r\n" % f"{retry_after:g}".encode()
+    return b"HTTP/1.1 %d %s\r\nContent-Type: application/json\r\n%sContent-Length: %d\r\n\r\n%s" % (
+        status, reason.encode(), extra, len(body), body)
 
 
 class SinkState:
@@ -50,6 +51,7 @@ class SinkState:
         self.fail_status = fail_status
         self.success_status = success_status
         self.fail_next: List[int] = []
+        self.retry_after: Optional[float] = None  # Retry-After header on injected failures
         self.rng = random.Random(seed)
         self.received: List[Tuple[int, bytes]] = []
         self.heads: List[bytes] = []
@@ -137,7 +139,7 @@ class _SinkProtocol(asyncio.Protocol):
                 fail = st.fail_status
             if fail is not None:
                 st.failed += 1
-                responses.append(_resp(fail, b'{"error":"injected"}'))
+                responses.append(_resp(fail, b'{"error":"injected"}', st.retry_after))
                 continue
             st.count += 1
             st.note(body)

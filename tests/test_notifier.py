@@ -112,6 +112,43 @@ def test_5xx_retried_4xx_not(pool_cls):
     assert m.c["notify_retried"] == 2 and m.c["notify_failed"] == 1 and m.c["notify_delivered"] == 1
 
 
+def test_retry_after_delays_the_retry(pool_cls):
+    # 429/503 with Retry-After: the retry waits what clusterapi asked for,
+    # not the 10 ms policy delay
+    async def body():
+        sink, pool, m = await with_pool(pool_cls, attempts=4)
+        sink.state.fail_next = [429, 503]
+        sink.state.retry_after = 0.2
+        t0 = time.monotonic()
+        pool.submit("a", "ADDED", "default", "a", core("a"), 0, TS)
+        pool.flush()
+        assert await pool.drain(5)
+        elapsed = time.monotonic() - t0
+        names = [p["name"] for p in sink.state.payloads()]
+        await close(sink, pool)
+        return names, m, elapsed
+
+    names, m, elapsed = run(body())
+    assert names == ["pod-a"]
+    assert elapsed >= 2 * 0.2 * 0.9
+    assert m.c["notify_retried"] == 2 and m.c["notify_retry_after_waits"] == 2
+
+
+@pytest.mark.parametrize("native", [False, True])
+def test_scanner_reports_retry_after(native):
+    from k8s_watcher_amd.net.http import response_scanner
+    sc = response_scanner(native)
+    out = sc.feed(b"HTTP/1.1 200 OK\r\nContent-Length: 0\r\n\r\n"
+                  b"HTTP/1.1 429 Too Many Requests\r\nRetry-After: 3\r\nContent-Length: 2\r\n\r\n{}"
+                  b"HTTP/1.1 503 Service Unavailable\r\nretry-after:  0.5 \r\nContent-Length: 0\r\n\r\n"
+                  b"HTTP/1.1 503 Service Unavailable\r\nRetry-After: 9999\r\nContent-Length: 0\r\n\r\n"
+                  b"HTTP/1.1 503 Service Unavailable\r\nRetry-After: Wed, 21 Oct 2015 07:28:00 GMT\r\n"
+                  b"Content-Length: 0\r\n\r\n"
+                  b"HTTP/1.1 500 Internal Server Error\r\nContent-Length: 0\r\n\r\n")
+    assert out == [200, (429, True, b"{}", 3.0), (503, True, b"", 0.5), (503, True, b"", 300.0),
+                   (503, True, b"", -1.0), (500, True, b"", -1.0)]
+
+
 def test_gives_up_after_max_attempts(pool_cls):
     async def body():
         sink, pool, m = await with_pool(pool_cls, {"fail_rate": 1.0}, attempts=3)
@@ -301,3 +338,40 @@ def test_rate_limit_paces_requests(pool_cls):
         assert sink.state.count == 50 and 0.15 <= took <= 1.5  # 40 beyond the burst at 200/s ~ 0.2 s
         await close(sink, pool)
     run(body())
+
+
+def test_compat_clients_honour_retry_after():
+    """The reference-compatible clients (sync and async) wait the sink's Retry-After."""
+    import threading
+
+    from k8s_watcher_amd.notify.clusterapi import AsyncClusterApiClient, ClusterApiClient
+
+    async def body():
+        sink = StubSink()
+        await sink.start()
+        sink.state.retry_after = 0.2
+        s = settings(sink.url, attempts=3)
+        sink.state.fail_next = [429]
+        ac = AsyncClusterApiClient.from_settings(s)
+        t0 = time.monotonic()
+        assert await ac.update_pod_status({"name": "a", "uid": "1"})
+        t_async = time.monotonic() - t0
+        sink.state.fail_next = [503]
+        sc = ClusterApiClient.from_settings(s)
+        out = {}
+
+        def post():
+            t1 = time.monotonic()
+            out["ok"] = sc.update_pod_status({"name": "b", "uid": "2"})
+            out["t"] = time.monotonic() - t1
+
+        t = threading.Thread(target=post)
+        t.start()
+        while t.is_alive():
+            await asyncio.sleep(0.01)
+        assert out["ok"] and sink.state.count == 2
+        await sink.stop()
+        return t_async, out["t"]
+
+    t_async, t_sync = run(body())
+    assert t_async >= 0.18 and t_sync >= 0.18
