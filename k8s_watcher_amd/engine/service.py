@@ -96,7 +96,8 @@ class WatcherService:
             ep = self.load_endpoint()
             self.endpoint = ep
             self.api = KubeApi(ep, timeout=self.settings.kubernetes.request_timeout,
-                               compression=self.settings.kubernetes.compression)
+                               compression=self.settings.kubernetes.compression,
+                               keepalive=self.settings.kubernetes.tcp_keepalive_seconds)
             ver = await self.api.get_version()
             self.server_version = ver.get("gitVersion") or f"{ver.get('major')}.{ver.get('minor')}"
             self.log.info(f"Successfully connected to Kubernetes API version: {self.server_version}")

@@ -45,7 +45,8 @@ def pods_path(namespace: Optional[str] = None) -> str:
 
 
 class KubeApi:
-    def __init__(self, endpoint: KubeEndpoint, timeout: float = 30.0, compression: bool = True) -> None:
+    def __init__(self, endpoint: KubeEndpoint, timeout: float = 30.0, compression: bool = True,
+                 keepalive: float = 30.0) -> None:
         self.endpoint = endpoint
         # LIST bodies of a large cluster shrink ~10x with gzip (the API server
         # compresses responses over 128 KiB when asked); watches stay uncompressed
@@ -54,7 +55,7 @@ class KubeApi:
         headers.update(endpoint.static_headers)
         self.http = HttpClient(endpoint.server, endpoint.ssl_context, headers=headers,
                                timeout=timeout, header_provider=endpoint.header_provider,
-                               server_name=endpoint.tls_server_name)
+                               server_name=endpoint.tls_server_name, keepalive=keepalive)
 
     async def _get(self, path: str, query: Optional[Dict[str, object]] = None,
                    timeout: Optional[float] = None, headers: Optional[Dict[str, str]] = None) -> Response:

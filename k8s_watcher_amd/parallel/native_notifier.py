@@ -220,7 +220,7 @@ class NativeNotifierPool:
             family, stype, proto, _, sa = await self._resolve()
             sock = socket.socket(family, stype, proto)
             sock.setblocking(False)
-            tune_socket(sock)
+            tune_socket(sock, self.settings.tcp_keepalive_seconds)
             await with_timeout(self.loop.sock_connect(sock, sa), self.settings.timeout)
         except (OSError, asyncio.TimeoutError) as exc:
             if sock is not None:

@@ -86,7 +86,7 @@ class _Conn(asyncio.Protocol):
     # ------------------------------------------------------------- asyncio protocol
     def connection_made(self, transport) -> None:  # type: ignore[override]
         self.transport = transport
-        tune_socket(transport.get_extra_info("socket"))
+        tune_socket(transport.get_extra_info("socket"), self.pool.settings.tcp_keepalive_seconds)
         self.state = self.UP
         self.connect_backoff.reset()
         self.scanner.reset()

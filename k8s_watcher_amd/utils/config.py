@@ -202,6 +202,7 @@ class KubernetesSettings:
     use_mock: bool = False
     request_timeout: float = 30.0
     compression: bool = True  # Accept-Encoding: gzip on LIST requests
+    tcp_keepalive_seconds: float = 30.0  # dead-peer detection on API-server sockets (net/sockopt.py); 0 = off
 
 
 @dataclass
@@ -244,6 +245,7 @@ class ClusterApiSettings:
     spool: SpoolSettings = field(default_factory=SpoolSettings)
     rate_limit_qps: float = 0.0  # clusterapi.rate_limit.qps; 0 = unlimited
     rate_limit_burst: float = 100.0
+    tcp_keepalive_seconds: float = 30.0  # dead-peer detection on clusterapi sockets (net/sockopt.py); 0 = off
 
 
 @dataclass
@@ -421,6 +423,8 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         use_mock=_as_bool(k.get("use_mock", False), "kubernetes.use_mock"),
         request_timeout=_as_float(k.get("request_timeout", 30.0), "kubernetes.request_timeout"),
         compression=_as_bool(k.get("compression", True), "kubernetes.compression"),
+        tcp_keepalive_seconds=max(0.0, _as_float(k.get("tcp_keepalive_seconds", 30.0),
+                                                 "kubernetes.tcp_keepalive_seconds")),
     )
 
     level = str(w.get("log_level", "INFO")).upper()
@@ -492,6 +496,8 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         rate_limit_qps=max(0.0, _as_float((c.get("rate_limit") or {}).get("qps", 0), "clusterapi.rate_limit.qps")),
         rate_limit_burst=max(1.0, _as_float((c.get("rate_limit") or {}).get("burst", 100),
                                             "clusterapi.rate_limit.burst")),
+        tcp_keepalive_seconds=max(0.0, _as_float(c.get("tcp_keepalive_seconds", 30.0),
+                                                 "clusterapi.tcp_keepalive_seconds")),
     )
 
     metrics = MetricsSettings(

@@ -71,3 +71,15 @@ def test_http_client_connections_are_tuned():
     o = asyncio.run(run())
     assert o["keepalive"] and (o["idle"], o["intvl"], o["cnt"]) == (12, 4, 3)
     assert o["user_timeout"] == 24_000
+
+
+def test_keepalive_settings():
+    from k8s_watcher_amd.utils.config import ConfigError, load_settings
+    s = load_settings("staging")
+    assert s.kubernetes.tcp_keepalive_seconds == 30 and s.clusterapi.tcp_keepalive_seconds == 30
+    s = load_settings("staging", overrides={"kubernetes": {"tcp_keepalive_seconds": 0},
+                                            "clusterapi": {"tcp_keepalive_seconds": 45}})
+    assert s.kubernetes.tcp_keepalive_seconds == 0 and s.clusterapi.tcp_keepalive_seconds == 45
+    import pytest
+    with pytest.raises(ConfigError):
+        load_settings("staging", overrides={"clusterapi": {"tcp_keepalive_seconds": "soon"}})
