@@ -106,10 +106,23 @@ class Reflector:
         events = []
         cont = None
         list_rv = None
+        limit: Optional[int] = w.list_page_size
         while True:
-            body = await self.api.list_pods_raw(
-                namespace=self.namespace, limit=w.list_page_size, continue_token=cont,
-                label_selector=w.label_selector, field_selector=w.field_selector)
+            try:
+                body = await self.api.list_pods_raw(
+                    namespace=self.namespace, limit=limit, continue_token=cont,
+                    label_selector=w.label_selector, field_selector=w.field_selector)
+            except ApiError as exc:
+                if exc.status != 410 or cont is None:
+                    raise
+                # the continue token outlived etcd's compaction window (a large
+                # cluster paged slowly): paging again would likely expire again,
+                # so take the state in one unpaginated LIST, as client-go's
+                # pager does (FullListIfExpired)
+                self.metrics.c["list_continue_expired"] += 1
+                self.log.warning("LIST continue token expired (410); retrying as one unpaginated LIST")
+                events, cont, list_rv, limit = [], None, None, None
+                continue
             page_rv, cont, evs = self.decoder.decode_list(body)
             if list_rv is None:
                 list_rv = page_rv

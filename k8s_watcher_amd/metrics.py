@@ -44,6 +44,7 @@ COUNTERS = (
     "api_throttled",        # 429 answers from the API server (not counted against watcher.retry)
     "retry_after_waits",    # retries delayed to the API server's Retry-After
     "relists",
+    "list_continue_expired",  # paginated LISTs whose continue token expired (redone unpaginated)
     "watch_list_syncs",     # initial state via WatchList (sendInitialEvents) instead of LIST
     "expired_410",
     "checkpoints_written",

@@ -150,6 +150,7 @@ class FakeApiServer:
         self.writers: Set[asyncio.StreamWriter] = set()
         self.fail_next: List[Tuple[int, str, Optional[float]]] = []
         self.empty_watches = 0
+        self.expire_continues = 0  # the next N paginated LIST continuations answer 410
         self.requests: List[Tuple[str, str]] = []
         self.server: Optional[asyncio.AbstractServer] = None
         self.port = 0
@@ -420,6 +421,12 @@ class FakeApiServer:
         pods = [p for (pns, _), p in sorted(self.pods.items())
                 if (ns is None or pns == ns) and _match_labels(p, q.get("labelSelector"))
                 and _match_fields(p, q.get("fieldSelector"))]
+        if q.get("continue") and self._continue_expired(q["continue"]):
+            # as the API server once etcd compacted past the token's revision
+            self._send_json(writer, 410, _status(
+                410, "Expired", "The provided continue parameter is too old to display a consistent "
+                "list result. You can start a new list without the continue parameter."), "Gone")
+            return True
         self._send_json(writer, 200, self._paginate("PodList", pods, q),
                         gzip_ok="gzip" in headers.get("accept-encoding", ""))
         return True
@@ -474,6 +481,15 @@ class FakeApiServer:
         self.leases[key] = obj
         self.lease_writes.append((key, copy.deepcopy(obj["spec"])))
         return copy.deepcopy(obj)
+
+    def _continue_expired(self, token: str) -> bool:
+        if self.expire_continues > 0:
+            self.expire_continues -= 1
+            return True
+        try:
+            return int(json.loads(base64.urlsafe_b64decode(token.encode()))["rv"]) < self.compacted_rv
+        except (ValueError, KeyError, TypeError):
+            return False
 
     def _paginate(self, kind: str, items: List[Dict[str, Any]], q: Dict[str, str]) -> Dict[str, Any]:
         start = 0

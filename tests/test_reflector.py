@@ -230,6 +230,63 @@ def test_retry_after_on_5xx_counts_as_failure_but_waits():
     run(body())
 
 
+def test_expired_list_continue_falls_back_to_one_unpaginated_list():
+    # a continue token that outlived etcd compaction (410 mid-pagination):
+    # the state is taken in one LIST without limit, each pod notified once
+    async def body():
+        async with Stack(overrides={"watcher": {"list_page_size": 2}}) as st:
+            f = st.factory
+            pods = [st.srv.create(f.running(f.new_pod())) for _ in range(7)]
+            st.srv.expire_continues = 1
+            svc = st.service()
+            await svc.start()
+            await st.settle(7)
+            got = st.delivered()
+            assert sorted(u for u, _, _ in got) == sorted(p["metadata"]["uid"] for p in pods)
+            assert {t for _, t, _ in got} == {"ADDED"}
+            assert svc.metrics.c["list_continue_expired"] == 1
+            assert svc.metrics.c["relists"] == 1
+            lists = [t for m, t in st.srv.requests if t.startswith("/api/v1/pods") and "watch=" not in t]
+            assert "limit=2" in lists[0] and "continue=" in lists[1] and "limit=" not in lists[2]
+            # and the watch resumes from the full list's resourceVersion
+            evs = lifecycle_apply(st, 1)
+            await st.settle(7 + len(evs))
+
+    run(body())
+
+
+def test_fake_apiserver_expires_continue_after_compaction():
+    import json as _json
+    import urllib.request
+
+    async def body():
+        srv = FakeApiServer()
+        await srv.start()
+        f = PodFactory(seed=3)
+        for _ in range(3):
+            srv.create(f.new_pod())
+        loop = asyncio.get_running_loop()
+
+        def get(url):
+            try:
+                with urllib.request.urlopen(url) as r:
+                    return r.status, _json.loads(r.read())
+            except urllib.error.HTTPError as e:
+                return e.code, _json.loads(e.read())
+
+        st1, page = await loop.run_in_executor(None, get, srv.url + "/api/v1/pods?limit=1")
+        tok = page["metadata"]["continue"]
+        st2, _ = await loop.run_in_executor(None, get, srv.url + "/api/v1/pods?limit=1&continue=" + tok)
+        srv.create(f.new_pod())
+        srv.compact()
+        st3, err = await loop.run_in_executor(None, get, srv.url + "/api/v1/pods?limit=1&continue=" + tok)
+        await srv.stop()
+        return st1, st2, st3, err
+
+    st1, st2, st3, err = run(body())
+    assert (st1, st2, st3) == (200, 200, 410) and err["reason"] == "Expired"
+
+
 def test_short_watches_back_off_without_failing():
     # a proxy that ends every watch at once: reconnects are paced by the
     # backoff (no hot loop) and do not spend the failure budget
