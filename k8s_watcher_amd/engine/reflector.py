@@ -370,6 +370,11 @@ class Reflector:
                     self.log.warning(f"Watch resourceVersion {self.rv} expired (410); relisting")
                     need_list = True
                     continue
+                if exc.status == 401 and self.api.endpoint.invalidate_credentials():
+                    # a rotated service-account token or an expired exec
+                    # credential: the next attempt fetches a fresh one
+                    self.metrics.c["auth_refreshes"] += 1
+                    self.log.warning("API server answered 401; refreshing credentials")
                 if exc.status == 429:
                     # throttled by API Priority and Fairness: wait as asked but
                     # do not count it toward max_attempts — exiting and

@@ -59,6 +59,17 @@ class KubeEndpoint:
             h.update(self.header_provider())
         return h
 
+    def invalidate_credentials(self) -> bool:
+        """After a ``401``: drop the cached token so the next request re-reads
+        the token file / re-runs the exec plugin (client-go does the same).
+        Returns False when the credentials are static (nothing to refresh)."""
+        owner = getattr(self.header_provider, "__self__", None)
+        inval = getattr(owner, "invalidate", None)
+        if inval is None:
+            return False
+        inval()
+        return True
+
 
 # --------------------------------------------------------------------------- helpers
 
@@ -198,6 +209,9 @@ class _ExecCredential:
             self._bg.start()
         return {"Authorization": f"Bearer {self._token}"} if self._token else {}
 
+    def invalidate(self) -> None:
+        self._token = None  # the next headers() runs the plugin in the foreground
+
     def _refresh_bg(self) -> None:
         try:
             self._refresh()
@@ -255,6 +269,9 @@ class _TokenFile:
             if not self._token:
                 raise ConfigException(f"cannot read token file {self.path}: {exc}") from None
         self._read_at = time.monotonic()
+
+    def invalidate(self) -> None:
+        self._read_at = float("-inf")  # re-read on the next request
 
     def headers(self) -> Dict[str, str]:
         if time.monotonic() - self._read_at > self.period:

@@ -41,6 +41,7 @@ COUNTERS = (
     "spool_dropped",
     "watch_restarts",
     "short_watches",        # watches the server ended at once with nothing in them (backed off)
+    "auth_refreshes",       # 401 answers that made the watcher re-read its token / re-run the exec plugin
     "api_throttled",        # 429 answers from the API server (not counted against watcher.retry)
     "retry_after_waits",    # retries delayed to the API server's Retry-After
     "relists",

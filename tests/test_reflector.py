@@ -413,3 +413,65 @@ def test_server_side_namespace_scope():
             assert any("/namespaces/default/pods" in t for _, t in st.srv.requests)
 
     run(body())
+
+
+def test_401_rereads_rotated_token_file(tmp_path):
+    # a rotated service-account / kubeconfig tokenFile: the 401 makes the
+    # watcher re-read the file at once instead of waiting for the 60 s period
+    from k8s_watcher_amd.kube.kubeconfig import load_kube_config
+
+    async def body():
+        async with Stack(server_kwargs={"token": "one"}) as st:
+            tok = tmp_path / "tok"
+            tok.write_text("one\n")
+            cfg = tmp_path / "cfg"
+            cfg.write_text(f"""
+current-context: x
+clusters: [{{name: c, cluster: {{server: "{st.srv.url}"}}}}]
+contexts: [{{name: x, context: {{cluster: c, user: u}}}}]
+users: [{{name: u, user: {{tokenFile: tok}}}}]
+""")
+            st.service()
+            svc = WatcherService(st.settings, endpoint=load_kube_config(str(cfg)), metrics=Metrics(True))
+            st.svc = svc
+            await svc.start()
+            first = lifecycle_apply(st, 1)
+            await st.settle(len(first))
+            st.srv.token = "two"
+            tok.write_text("two\n")
+            st.srv.drop_connections()
+            second = lifecycle_apply(st, 1)
+            await st.settle(len(first) + len(second))
+            assert_exactly_once(st.delivered(), first + second)
+            assert svc.metrics.c["auth_refreshes"] >= 1
+
+    run(body())
+
+
+def test_invalidate_credentials_static_and_exec(tmp_path):
+    import sys
+
+    from k8s_watcher_amd.kube.kubeconfig import load_kube_config
+    counter = tmp_path / "n"
+    counter.write_text("0")
+    plugin = tmp_path / "plugin.py"
+    plugin.write_text(
+        "import json,pathlib\np=pathlib.Path(%r)\nn=int(p.read_text())+1\np.write_text(str(n))\n"
+        "print(json.dumps({'apiVersion':'client.authentication.k8s.io/v1beta1','kind':'ExecCredential',"
+        "'status':{'token':'t%%d' %% n}}))\n" % str(counter))
+    cfg = tmp_path / "cfg"
+    cfg.write_text(f"""
+current-context: x
+clusters: [{{name: c, cluster: {{server: "http://h"}}}}]
+contexts: [{{name: x, context: {{cluster: c, user: u}}}}]
+users:
+- name: u
+  user:
+    exec: {{apiVersion: client.authentication.k8s.io/v1beta1, command: "{sys.executable}", args: ["{plugin}"]}}
+""")
+    ep = load_kube_config(str(cfg))
+    assert ep.auth_headers() == {"Authorization": "Bearer t1"}
+    assert ep.auth_headers() == {"Authorization": "Bearer t1"}  # cached
+    assert ep.invalidate_credentials()
+    assert ep.auth_headers() == {"Authorization": "Bearer t2"}
+    assert not KubeEndpoint(server="http://h", static_headers={"Authorization": "Bearer s"}).invalidate_credentials()
