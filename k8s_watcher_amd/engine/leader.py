@@ -163,17 +163,45 @@ class LeaderElector:
 
     # ------------------------------------------------------------------ one round
     async def try_acquire_or_renew(self) -> bool:
-        """One compare-and-swap round; True if this candidate holds the lease afterwards."""
-        now_wall = time.time()
-        timeout = self.s.renew_deadline_seconds
+        """One compare-and-swap round; True if this candidate holds the lease afterwards.
+
+        The whole round (GET, then PUT or POST, with any keep-alive retry)
+        runs under ONE deadline, as client-go's ``renew`` does: for a leader,
+        what is left of ``renew_deadline_seconds`` since its last successful
+        renew; for a candidate, the full deadline. Per-request timeouts alone
+        would let a round outlast the lease (each request gets the deadline
+        for connect and again for the response), and a candidate takes the
+        lease ``lease_duration_seconds`` after the last renew — two leaders.
+        The caller (:meth:`run`) steps down when a leader's round fails, so
+        a leader stops acting strictly before its lease can expire.
+        """
+        budget = self.s.renew_deadline_seconds
+        if self._leader:
+            budget = min(budget, self.last_renew + self.s.renew_deadline_seconds - self.clock())
+            if budget <= 0:
+                return False
+        deadline = time.monotonic() + budget
         try:
-            lease = await self.api.get_lease(self.namespace, self.name, timeout=timeout)
+            return await asyncio.wait_for(self._round(deadline), budget)
+        except asyncio.TimeoutError:
+            self.metrics.c["lease_update_errors"] += 1
+            self.log.warning(f"Lease {self.namespace}/{self.name} round exceeded its {budget:.2f}s deadline")
+            return False
+
+    async def _round(self, deadline: float) -> bool:
+        now_wall = time.time()
+
+        def left() -> float:
+            return max(0.001, deadline - time.monotonic())
+
+        try:
+            lease = await self.api.get_lease(self.namespace, self.name, timeout=left())
             if lease is None:
                 rec = LeaderRecord(holder=self.identity, lease_duration=int(round(self.s.lease_duration_seconds)),
                                    acquire_time=micro_time(now_wall), renew_time=micro_time(now_wall))
                 body = {"apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
                         "metadata": {"name": self.name, "namespace": self.namespace}, "spec": rec.spec()}
-                created = await self.api.create_lease(self.namespace, body, timeout=timeout)
+                created = await self.api.create_lease(self.namespace, body, timeout=left())
                 self._observe(rec, (created.get("metadata") or {}).get("resourceVersion"))
                 self.last_renew = self.clock()
                 return True
@@ -195,16 +223,21 @@ class LeaderElector:
             lease = dict(lease)
             lease["metadata"] = dict(md)
             lease["spec"] = rec.spec()
-            updated = await self.api.replace_lease(self.namespace, self.name, lease, timeout=timeout)
+            updated = await self.api.replace_lease(self.namespace, self.name, lease, timeout=left())
             self._observe(rec, (updated.get("metadata") or {}).get("resourceVersion"))
             self.last_renew = self.clock()
             return True
         except ApiError as exc:
+            if exc.status == 401 and await self.api.endpoint.refresh_credentials():
+                # a standby runs no reflector, so nothing else would refresh its
+                # credentials: without this a rotated token locks it out for good
+                self.metrics.c["auth_refreshes"] += 1
+                self.log.warning("API server answered 401 to a lease request; refreshing credentials")
             if exc.status not in (404, 409):
                 self.log.warning(f"Lease {self.namespace}/{self.name} update failed: {exc}")
             self.metrics.c["lease_update_conflicts" if exc.status == 409 else "lease_update_errors"] += 1
             return False
-        except (HttpError, OSError, asyncio.TimeoutError, ValueError) as exc:
+        except (HttpError, OSError, ValueError) as exc:
             self.metrics.c["lease_update_errors"] += 1
             self.log.warning(f"Lease {self.namespace}/{self.name} update failed: {exc}")
             return False

@@ -201,9 +201,10 @@ class Reflector:
                 label_selector=w.label_selector, field_selector=w.field_selector,
                 raw_chunked=True, on_mode=on_mode)
         except ApiError as exc:
-            if exc.status == 410:
-                raise
-            if 400 <= exc.status < 500:
+            # only the answers that mean "no such feature" downgrade to LIST for
+            # good; 401 (token rotation), 403, 410 and 429 (APF throttling) go
+            # to run() for credential refresh, relist and Retry-After handling
+            if exc.status in (400, 404, 405, 415, 422, 501):
                 raise WatchListUnsupported(str(exc)) from None
             raise
         try:
@@ -332,6 +333,12 @@ class Reflector:
     async def run(self) -> None:
         w = self.settings.watcher
         backoff = Backoff(w.retry)
+        # consecutive 410 → relist cycles in which the watch never got past the
+        # relist's resourceVersion (a lagging watch cache, a relist RV that is
+        # already compacted): each further relist waits longer, as client-go's
+        # ListAndWatch backoff does, instead of LIST-storming the API server
+        expired_backoff = Backoff(w.retry)
+        relist_rv: Optional[str] = None
         need_list = self.rv is None
         first = not self.primed
         failures = 0
@@ -342,6 +349,7 @@ class Reflector:
                     await self.sync(notify=notify)
                     need_list = False
                     first = False
+                    relist_rv = self.rv
                 else:
                     self.synced.set()
                 rv_before, t0 = self.rv, time.monotonic()
@@ -349,6 +357,8 @@ class Reflector:
                 if self._stop.is_set():
                     break
                 self.metrics.c["watch_restarts"] += 1
+                if self.rv != relist_rv:
+                    expired_backoff.reset()
                 if time.monotonic() - t0 < SHORT_WATCH_SECONDS and self.rv == rv_before:
                     # the server ended the watch at once with nothing in it
                     # (proxy or API server misbehaving): back off instead of
@@ -359,31 +369,35 @@ class Reflector:
                     continue
                 failures = 0
                 backoff.reset()
-            except Expired:
+            except (Expired, ApiError) as exc:
+                if isinstance(exc, ApiError) and exc.status != 410:
+                    if exc.status == 401 and await self.api.endpoint.refresh_credentials():
+                        # a rotated service-account token or an expired exec
+                        # credential: the next attempt fetches a fresh one
+                        self.metrics.c["auth_refreshes"] += 1
+                        self.log.warning("API server answered 401; refreshing credentials")
+                    if exc.status == 429:
+                        # throttled by API Priority and Fairness: wait as asked but
+                        # do not count it toward max_attempts — exiting and
+                        # relisting would only add load to a busy API server
+                        self.metrics.c["api_throttled"] += 1
+                        await self._backoff(backoff, 0, exc)
+                        continue
+                    failures += 1
+                    await self._backoff(backoff, failures, exc)
+                    continue
                 self.metrics.c["expired_410"] += 1
-                self.log.warning(f"Watch resourceVersion {self.rv} expired (410); relisting")
-                need_list = True
                 failures = 0
-            except ApiError as exc:
-                if exc.status == 410:
-                    self.metrics.c["expired_410"] += 1
+                if relist_rv is not None and self.rv == relist_rv:
+                    # expired again without a single event past the last relist
+                    delay = expired_backoff.next_delay()
+                    self.metrics.c["expired_relist_backoffs"] += 1
+                    self.log.warning(f"Watch resourceVersion {self.rv} expired (410) again right after a "
+                                     f"relist; relisting in {delay:.2f}s")
+                    await self._sleep(delay)
+                else:
                     self.log.warning(f"Watch resourceVersion {self.rv} expired (410); relisting")
-                    need_list = True
-                    continue
-                if exc.status == 401 and self.api.endpoint.invalidate_credentials():
-                    # a rotated service-account token or an expired exec
-                    # credential: the next attempt fetches a fresh one
-                    self.metrics.c["auth_refreshes"] += 1
-                    self.log.warning("API server answered 401; refreshing credentials")
-                if exc.status == 429:
-                    # throttled by API Priority and Fairness: wait as asked but
-                    # do not count it toward max_attempts — exiting and
-                    # relisting would only add load to a busy API server
-                    self.metrics.c["api_throttled"] += 1
-                    await self._backoff(backoff, 0, exc)
-                    continue
-                failures += 1
-                await self._backoff(backoff, failures, exc)
+                need_list = True
             except HttpError as exc:
                 if self._stop.is_set():
                     break

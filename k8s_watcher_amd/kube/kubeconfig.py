@@ -35,11 +35,19 @@ from typing import Any, Callable, Dict, List, Optional, Tuple
 
 import yaml
 
+from ..net.http import HttpError
+
 SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
 
 
 class ConfigException(Exception):
     """Same role as ``kubernetes.config.ConfigException`` (``pod_watcher.py:2,152``)."""
+
+
+class CredentialError(ConfigException, HttpError):
+    """The exec credential plugin failed while serving a request. A
+    :class:`ConfigException` at setup time; at run time an :class:`HttpError`,
+    so the reflector backs off and retries instead of ending the watch."""
 
 
 @dataclass
@@ -62,12 +70,26 @@ class KubeEndpoint:
     def invalidate_credentials(self) -> bool:
         """After a ``401``: drop the cached token so the next request re-reads
         the token file / re-runs the exec plugin (client-go does the same).
+        An exec plugin is re-run on a background thread, keeping the old token
+        until the new one arrives: the event loop never waits for the plugin.
         Returns False when the credentials are static (nothing to refresh)."""
         owner = getattr(self.header_provider, "__self__", None)
         inval = getattr(owner, "invalidate", None)
         if inval is None:
             return False
         inval()
+        return True
+
+    async def refresh_credentials(self) -> bool:
+        """:meth:`invalidate_credentials`, then wait (off the event loop) until
+        the fresh token is in place. False when there is nothing to refresh."""
+        if not self.invalidate_credentials():
+            return False
+        owner = getattr(self.header_provider, "__self__", None)
+        wait = getattr(owner, "wait_refreshed", None)
+        if wait is not None:
+            import asyncio
+            await asyncio.get_running_loop().run_in_executor(None, wait)
         return True
 
 
@@ -190,35 +212,63 @@ def build_ssl_context(ca_file: Optional[str] = None, ca_data: Optional[bytes] = 
 
 
 class _ExecCredential:
-    """Runs a client-go ``exec`` credential plugin and caches its token."""
+    """Runs a client-go ``exec`` credential plugin and caches its token.
+
+    Only the very first request waits for the plugin in the foreground
+    (there is no token to send). Afterwards every refresh — ahead of the
+    expiry, after a ``401`` (:meth:`invalidate`) or once the token expired —
+    runs on one background thread while requests keep the last token; a
+    failing plugin keeps the old token and surfaces as a retryable
+    :class:`CredentialError`, never as a crash of the watch loop.
+    """
 
     def __init__(self, spec: Dict[str, Any], base: str = "") -> None:
         self.spec = spec
         self.base = base  # a relative command path resolves against the kubeconfig's directory
         self._token: Optional[str] = None
         self._expiry: float = 0.0
+        self._lock = threading.Lock()
         self._bg: Optional[threading.Thread] = None
+        self.last_error: Optional[str] = None
+        self.refreshes = 0
 
     def headers(self) -> Dict[str, str]:
-        now = time.time()
-        if self._token is None or (self._expiry and now >= self._expiry - 10):
-            self._refresh()  # no usable token: the request has to wait for the plugin
-        elif self._expiry and now >= self._expiry - 120 and self._bg is None:
-            # still valid: refresh on a thread so the event loop does not block on the plugin
-            self._bg = threading.Thread(target=self._refresh_bg, daemon=True)
-            self._bg.start()
+        if self._token is None:
+            try:
+                self._refresh()  # nothing to send yet: this one request waits for the plugin
+            except ConfigException as exc:
+                raise CredentialError(str(exc)) from None
+        elif self._expiry and time.time() >= self._expiry - 120:
+            self._start_bg()  # refresh ahead of (or after) the expiry, off the event loop
         return {"Authorization": f"Bearer {self._token}"} if self._token else {}
 
     def invalidate(self) -> None:
-        self._token = None  # the next headers() runs the plugin in the foreground
+        """A ``401``: re-run the plugin in the background, keep the old token meanwhile."""
+        if self._token is None:
+            return  # the next headers() runs it anyway
+        self._start_bg()
+
+    def wait_refreshed(self, timeout: float = 90.0) -> None:
+        """Block (call from an executor thread) until a running refresh ends."""
+        th = self._bg
+        if th is not None:
+            th.join(timeout)
+
+    def _start_bg(self) -> None:
+        with self._lock:
+            if self._bg is not None:
+                return
+            self._bg = threading.Thread(target=self._refresh_bg, name="exec-credential", daemon=True)
+            self._bg.start()
 
     def _refresh_bg(self) -> None:
         try:
             self._refresh()
-        except ConfigException:
-            pass  # retried in the foreground once the current token expires
+        except ConfigException as exc:
+            self.last_error = str(exc)  # keep the old token; the next 401 or expiry check retries
         finally:
-            self._bg = None
+            with self._lock:
+                self._bg = None
 
     def _refresh(self) -> None:
         cmd = [self.spec.get("command")] + list(self.spec.get("args") or [])
@@ -241,14 +291,19 @@ class _ExecCredential:
             status = json.loads(out).get("status") or {}
         except ValueError:
             raise ConfigException("exec credential plugin returned invalid JSON") from None
-        self._token = status.get("token")
+        token = status.get("token")
+        if not token:
+            raise ConfigException("exec credential plugin returned no token")
+        expiry = 0.0
         exp = status.get("expirationTimestamp")
-        self._expiry = 0.0
         if exp:
             from ..utils.timefmt import parse_k8s_time
             dt = parse_k8s_time(exp)
             if dt is not None:
-                self._expiry = dt.timestamp()
+                expiry = dt.timestamp()
+        self._token, self._expiry = token, expiry  # one assignment: a reader sees old or new, never half
+        self.last_error = None
+        self.refreshes += 1
 
 
 class _TokenFile:

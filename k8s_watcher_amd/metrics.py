@@ -48,6 +48,7 @@ COUNTERS = (
     "list_continue_expired",  # paginated LISTs whose continue token expired (redone unpaginated)
     "watch_list_syncs",     # initial state via WatchList (sendInitialEvents) instead of LIST
     "expired_410",
+    "expired_relist_backoffs",  # 410s right after a relist (no progress): the next relist waited
     "checkpoints_written",
     "leader_acquired",      # leadership terms started (engine/leader.py)
     "leader_lost",

@@ -161,6 +161,8 @@ class FakeApiServer:
         self.leases: Dict[Tuple[str, str], Dict[str, Any]] = {}
         self.lease_writes: List[Tuple[Tuple[str, str], Dict[str, Any]]] = []
         self.lease_fault: Optional[int] = None  # answer every lease request with this status
+        self.lease_stall = 0.0  # seconds every lease request waits before it is answered
+        self.expire_every_watch = False  # a lagging watch cache: every watch with an RV gets 410
 
     # ------------------------------------------------------------------ lifecycle
     async def start(self, host: str = "127.0.0.1", port: int = 0, ssl_context=None) -> int:
@@ -392,6 +394,8 @@ class FakeApiServer:
             self._send_json(writer, 201, doc, "Created")
             return True
         if path.startswith(LEASES_PREFIX):
+            if self.lease_stall:
+                await asyncio.sleep(self.lease_stall)
             code, doc = self._lease(method, path[len(LEASES_PREFIX):], body)
             self._send_json(writer, code, doc, _REASONS.get(code, "OK"))
             return True
@@ -527,7 +531,7 @@ class FakeApiServer:
                 since = int(rv_param)
             except ValueError:
                 since = -1
-            if since < self.compacted_rv:
+            if since < self.compacted_rv or self.expire_every_watch:
                 if self.expired_as_http_status:
                     self._send_json(writer, 410, _status(410, "Expired", "too old resource version"), "Gone")
                     await writer.drain()

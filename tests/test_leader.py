@@ -144,6 +144,72 @@ def test_release_hands_over_immediately_and_renew_deadline_steps_down():
     run(body(), timeout=30)
 
 
+def test_stalled_lease_requests_step_down_within_renew_deadline():
+    """A renew round is bounded by ONE deadline (what is left of
+    renew_deadline since the last renew), not by per-request timeouts: with
+    every lease request stalled, the leader stops leading before its lease
+    could expire for the others — even while its request is still in flight."""
+    async def body():
+        srv = FakeApiServer()
+        await srv.start()
+        api = KubeApi(KubeEndpoint(server=srv.url), timeout=30)
+        a = LeaderElector(api, le_settings("a", lease_duration_seconds=3, renew_deadline_seconds=1.0,
+                                           retry_period_seconds=0.2))
+        ta = asyncio.ensure_future(a.run())
+        await asyncio.wait_for(a.became_leader.wait(), 5)
+        await asyncio.sleep(0.3)
+        srv.lease_stall = 30.0  # the API server accepts the request and never answers in time
+        t_stall = asyncio.get_running_loop().time()
+        await asyncio.wait_for(a.lost.wait(), 3)
+        lost_after = asyncio.get_running_loop().time() - t_stall
+        # stepped down within renew_deadline of the last renew (+ scheduling slack),
+        # well before lease_duration (3 s) after it
+        assert lost_after < 1.3, lost_after
+        assert a.metrics.c["lease_update_errors"] >= 1
+        srv.lease_stall = 0.0
+        a.stop()
+        ta.cancel()
+        try:
+            await ta
+        except asyncio.CancelledError:
+            pass
+        await api.close()
+        await srv.stop()
+    run(body(), timeout=30)
+
+
+def test_standby_refreshes_credentials_on_401(tmp_path):
+    """A standby runs no reflector; its elector must refresh a rotated token
+    itself on a 401, or it could never take over."""
+    from k8s_watcher_amd.kube.kubeconfig import load_kube_config
+
+    async def body():
+        srv = FakeApiServer(token="one")
+        await srv.start()
+        tok = tmp_path / "tok"
+        tok.write_text("one\n")
+        cfg = tmp_path / "cfg"
+        cfg.write_text(f"""
+current-context: x
+clusters: [{{name: c, cluster: {{server: "{srv.url}"}}}}]
+contexts: [{{name: x, context: {{cluster: c, user: u}}}}]
+users: [{{name: u, user: {{tokenFile: tok}}}}]
+""")
+        api = KubeApi(load_kube_config(str(cfg)))
+        b = LeaderElector(api, le_settings("b"))
+        try:
+            assert await b.try_acquire_or_renew()
+            srv.token = "two"
+            tok.write_text("two\n")
+            assert not await b.try_acquire_or_renew()  # 401: refreshes (token file re-read)
+            assert b.metrics.c["auth_refreshes"] == 1
+            assert await b.try_acquire_or_renew()
+        finally:
+            await api.close()
+            await srv.stop()
+    run(body())
+
+
 def test_settings_validation():
     s = load_settings("development", overrides={"watcher": {"leader_election": {"enabled": True}}})
     le = s.watcher.leader_election

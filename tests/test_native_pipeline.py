@@ -3,6 +3,7 @@
 counters, same control events, for every filter combination."""
 
 import json
+import os
 import random
 
 import pytest
@@ -164,23 +165,38 @@ def test_decode_pool_matches_serial(threads):
 
 
 def test_decode_pool_lifecycle():
-    """Pools are created and joined with their pipelines (no leaked threads)."""
-    import os
-    from k8s_watcher_amd.ops.native import load
-    mod = load()
-
-    def os_threads():
-        return len(os.listdir("/proc/self/task"))
-
-    before = os_threads()
-    for _ in range(20):
-        pl = mod.Pipeline("production", mod.PodCache(), {}, None, True, False, 1, 0, True, True, None, False, False, 3)
-        assert os_threads() == before + 3
-        pl.feed(stream(), 0)
-        del pl
-    assert os_threads() == before
-    with pytest.raises(ValueError):
-        mod.Pipeline("production", mod.PodCache(), {}, None, True, False, 1, 0, True, True, None, False, False, 65)
+    """Pools are created and joined with their pipelines (no leaked threads).
+    Counted in a child process: threads other tests left behind in this
+    process may exit while we count."""
+    import subprocess
+    import sys
+    code = ("import os, sys; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+            "from k8s_watcher_amd.ops.native import load\n"
+            "from test_native_pipeline import stream\n"
+            "mod = load()\n"
+            "import time\n"
+            "def n(want=None):\n"
+            "    # a joined thread can linger in /proc for a moment after pthread_join returns\n"
+            "    for _ in range(200):\n"
+            "        c = len(os.listdir('/proc/self/task'))\n"
+            "        if want is None or c == want: return c\n"
+            "        time.sleep(0.005)\n"
+            "    return c\n"
+            "before = n()\n"
+            "for _ in range(20):\n"
+            "    pl = mod.Pipeline('production', mod.PodCache(), {}, None, True, False, 1, 0, True, True,"
+            " None, False, False, 3)\n"
+            "    assert n(before + 3) == before + 3, (n(), before)\n"
+            "    pl.feed(stream(), 0)\n"
+            "    del pl\n"
+            "assert n(before) == before, (n(), before)\n"
+            "try:\n"
+            "    mod.Pipeline('production', mod.PodCache(), {}, None, True, False, 1, 0, True, True, None,"
+            " False, False, 65)\n"
+            "except ValueError:\n"
+            "    print('ok')\n") % (ROOT, os.path.join(ROOT, "tests"))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stderr
 
 
 def test_decode_pool_create_destroy_race():

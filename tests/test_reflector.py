@@ -3,6 +3,7 @@ bookmarks, retries, checkpoint restart — each asserting exactly-once delivery.
 
 import asyncio
 import collections
+import math
 import time
 
 import pytest
@@ -115,6 +116,38 @@ def test_410_relists_and_diffs_against_cache(as_http_status):
             assert svc.metrics.c["expired_410"] >= 1 and svc.metrics.c["relists"] == 2
             # unchanged pods were not re-notified
             assert [u for u, _, _ in got].count(keep[0]["metadata"]["uid"]) == 1
+
+    run(body())
+
+
+@pytest.mark.parametrize("as_http_status", [False, True])
+def test_repeated_410_relists_back_off(as_http_status):
+    """An API server that answers every watch with 410 (a watch cache lagging
+    behind etcd) must not be LIST-stormed: consecutive relists that make no
+    progress wait exponentially longer (reflector.run, expired_backoff)."""
+    async def body():
+        async with Stack(server_kwargs={"expired_as_http_status": as_http_status}) as st:
+            f = st.factory
+            st.srv.create(f.running(f.new_pod()))
+            svc = st.service({"watcher": {"retry": {"delay_seconds": 0.1, "multiplier": 2.0,
+                                                    "max_delay_seconds": 30, "jitter": 0}}})
+            st.srv.expire_every_watch = True
+            await svc.start()
+            t0 = time.monotonic()
+            await asyncio.sleep(3.0)
+            elapsed = time.monotonic() - t0
+            lists = [t for m, t in st.srv.requests if t.startswith("/api/v1/pods") and "watch=" not in t]
+            # delays 0.1, 0.2, 0.4, 0.8, 1.6 s: at most 1 + log2(elapsed / 0.1 + 1) relists
+            assert 3 <= len(lists) <= 2 + math.log2(elapsed / 0.1 + 1), (len(lists), elapsed)
+            assert svc.metrics.c["expired_relist_backoffs"] >= len(lists) - 2
+            # the pod was notified exactly once: relists diff against the cache
+            await svc.notifier.drain(5)
+            assert len(st.sink.state.payloads()) == 1
+            # progress resets the backoff: a healthy watch after the storm resumes at once
+            st.srv.expire_every_watch = False
+            await asyncio.sleep(2.0)
+            st.srv.create(f.running(f.new_pod()))
+            await st.settle(2, timeout=10)
 
     run(body())
 
@@ -472,6 +505,73 @@ users:
     ep = load_kube_config(str(cfg))
     assert ep.auth_headers() == {"Authorization": "Bearer t1"}
     assert ep.auth_headers() == {"Authorization": "Bearer t1"}  # cached
-    assert ep.invalidate_credentials()
+    assert ep.invalidate_credentials()  # re-runs the plugin on a thread, old token meanwhile
+    ep.header_provider.__self__.wait_refreshed()
     assert ep.auth_headers() == {"Authorization": "Bearer t2"}
     assert not KubeEndpoint(server="http://h", static_headers={"Authorization": "Bearer s"}).invalidate_credentials()
+
+
+def _exec_kubeconfig(tmp_path, server_url, script):
+    import sys
+    plugin = tmp_path / "plugin.py"
+    plugin.write_text(script)
+    cfg = tmp_path / "cfg"
+    cfg.write_text(f"""
+current-context: x
+clusters: [{{name: c, cluster: {{server: "{server_url}"}}}}]
+contexts: [{{name: x, context: {{cluster: c, user: u}}}}]
+users:
+- name: u
+  user:
+    exec: {{apiVersion: client.authentication.k8s.io/v1beta1, command: "{sys.executable}", args: ["{plugin}"]}}
+""")
+    return cfg
+
+
+def test_401_reruns_exec_plugin_off_the_event_loop(tmp_path):
+    """A 401 re-runs the exec credential plugin on a thread: the event loop
+    keeps running while the (slow) plugin works, and a failing plugin is a
+    retried watch failure, not the end of the watcher."""
+    from k8s_watcher_amd.kube.kubeconfig import load_kube_config
+    state = tmp_path / "state"
+    state.write_text("0 ok")
+    script = ("import json, pathlib, sys, time\n"
+              "p = pathlib.Path(%r)\n"
+              "n, mode = p.read_text().split()\n"
+              "n = int(n) + 1\n"
+              "p.write_text(f'{n} {mode}')\n"
+              "if n > 1: time.sleep(0.6)\n"
+              "if mode == 'fail': sys.exit(3)\n"
+              "print(json.dumps({'apiVersion': 'client.authentication.k8s.io/v1beta1', 'kind': 'ExecCredential',"
+              " 'status': {'token': 'tok-%%s' %% (1 if n == 1 else 2)}}))\n") % str(state)
+
+    async def body():
+        async with Stack(server_kwargs={"token": "tok-1"}) as st:
+            cfg = _exec_kubeconfig(tmp_path, st.srv.url, script)
+            st.service({"watcher": {"retry": {"delay_seconds": 0.05, "max_attempts": 0}}})
+            svc = WatcherService(st.settings, endpoint=load_kube_config(str(cfg)), metrics=Metrics(True))
+            st.svc = svc
+            await svc.start()
+            first = lifecycle_apply(st, 1)
+            await st.settle(len(first))
+            # the token is revoked and the plugin starts failing for a while
+            state.write_text(state.read_text().split()[0] + " fail")
+            st.srv.token = "tok-2"
+            st.srv.drop_connections()
+            gaps, last = [], time.monotonic()
+            t_end = time.monotonic() + 2.0
+            while time.monotonic() < t_end:
+                await asyncio.sleep(0.01)
+                now = time.monotonic()
+                gaps.append(now - last)
+                last = now
+            # the plugin sleeps 0.6 s per run: none of it was spent on the loop
+            assert max(gaps) < 0.3, max(gaps)
+            assert not any(t.done() for t in svc._tasks)  # the reflector is still retrying
+            state.write_text(state.read_text().split()[0] + " ok")
+            second = lifecycle_apply(st, 1)
+            await st.settle(len(first) + len(second), timeout=20)
+            assert_exactly_once(st.delivered(), first + second)
+            assert svc.metrics.c["auth_refreshes"] >= 2
+
+    run(body(), timeout=60)

@@ -124,3 +124,28 @@ def test_gzip_list(compression):
         await sink.stop()
         await srv.stop()
     run(body())
+
+
+@pytest.mark.parametrize("status", [429, 401, 503])
+def test_watch_list_transient_errors_keep_watch_list(status):
+    """A throttled (429), unauthorised (401) or unavailable (503) WatchList
+    request is retried as a WatchList — only "feature missing" answers
+    (400/422...) downgrade the reflector to LIST for the rest of the process."""
+    async def body():
+        f = PodFactory(seed=25, namespaces=["default"])
+        pods = [f.running(f.new_pod()) for _ in range(3)]
+        ov = {"watcher": {**WL["watcher"], "retry": {"delay_seconds": 0.05, "max_attempts": 0}}}
+        srv, sink, svc = await start_stack("staging", overrides=ov, pods=pods)
+        srv.fail_requests(1, status, path_prefix="/api/v1/pods", retry_after=0.1 if status == 429 else None)
+        await svc.start()
+        await sink.state.wait_for(3, timeout=10)
+        assert svc.reflectors[0].watch_list is True
+        assert svc.metrics.c["watch_list_syncs"] == 1 and svc.metrics.c["relists"] == 1
+        assert not any("watch" not in t and "/pods" in t for _, t in srv.requests)  # never a LIST
+        if status == 429:
+            assert svc.metrics.c["api_throttled"] == 1
+        svc.stop()
+        await svc.shutdown()
+        await sink.stop()
+        await srv.stop()
+    run(body())
