@@ -26,7 +26,7 @@ from ..ops.decode import (ADDED, BOOKMARK, DELETED, E_EXTRA, E_HAS_STATUS, E_NAM
                           E_RV, E_TYPE, E_UID, MODIFIED)
 from ..ops.filters import TERMINAL_PHASES
 from ..parallel.shard import ShardFilter
-from ..utils.config import Settings
+from ..utils.config import Settings, ShardSettings
 from ..utils.fastlog import EventLog
 from ..utils.logsetup import SERVICE_LOGGER
 from ..utils.timefmt import event_timestamp
@@ -36,7 +36,8 @@ _POD_EVENTS = frozenset({ADDED, MODIFIED, DELETED})
 
 class EventPipeline:
     def __init__(self, settings: Settings, decoder, notifier, metrics: Metrics,
-                 cache: Optional[PodCache] = None, event_log: Optional[EventLog] = None) -> None:
+                 cache: Optional[PodCache] = None, event_log: Optional[EventLog] = None,
+                 event_sharding: bool = True) -> None:
         w = settings.watcher
         self.settings = settings
         self.decoder = decoder
@@ -50,7 +51,9 @@ class EventPipeline:
         self.phase_mode = w.notify_on == "phase_change"
         self.ts_mode = w.event_timestamp
         self.log_events_setting = w.log_events
-        self.shard = ShardFilter(w.shard)
+        # event_sharding=False: the watch scopes are already this shard's
+        # namespaces (parallel/shard.py), so every received event is ours
+        self.shard = ShardFilter(w.shard if event_sharding else ShardSettings())
         self.last_rv: Optional[str] = None
         self.native = None
         self._native_log = None

@@ -17,7 +17,10 @@ messages (§2.4) are emitted in the same order; the behavioural fixes are:
 With ``watcher.namespace_scope: server`` one reflector per target namespace
 watches ``/api/v1/namespaces/<ns>/pods``, so the API server only sends the
 pods the watcher cares about (the reference always watches the whole cluster
-and filters client-side).
+and filters client-side). With ``namespace_scope: discover`` the
+namespace set itself is watched (``engine/namespaces.py``) and one reflector
+runs per namespace this shard owns — the sharded form of the reference's
+all-namespaces watch: reflectors start and stop as namespaces come and go.
 """
 
 from __future__ import annotations
@@ -26,7 +29,7 @@ import asyncio
 import logging
 import os
 import time
-from typing import List, Optional
+from typing import Dict, List, Optional, Set
 
 from ..kube.api import ApiError, KubeApi
 from ..kube.kubeconfig import ConfigException, KubeEndpoint, load_incluster_config, load_kube_config
@@ -42,6 +45,7 @@ from ..utils.config import Settings
 from ..utils.fastlog import EventLog
 from ..utils.logsetup import SERVICE_LOGGER
 from .checkpoint import load_checkpoint, save_checkpoint
+from .namespaces import NamespaceWatcher
 from .pipeline import EventPipeline
 from .reflector import Reflector, WatchFailed
 
@@ -72,6 +76,12 @@ class WatcherService:
         self.server_version: Optional[str] = None
         self.spool = None
         self.spool_replayer = None
+        self.ns_watcher: Optional[NamespaceWatcher] = None
+        self._scope_tasks: Dict[str, asyncio.Task] = {}
+        self._failure: Optional[asyncio.Future] = None
+        self._saved_rvs: Dict[str, Optional[str]] = {}
+        self._multi = False  # several (or dynamic) watch scopes, each with its own pipeline
+        self._live = False  # scopes follow namespace changes once start() has built the first set
 
     # ------------------------------------------------------------------ setup
     def load_endpoint(self) -> KubeEndpoint:
@@ -214,8 +224,25 @@ class WatcherService:
             self._tasks.append(asyncio.ensure_future(self.spool_replayer.run()))
         self.decoder = make_decoder(s.watcher.engine, s.environment, s.watcher.state_format,
                                     s.watcher.payload_extra)
-        scopes = (ShardFilter(s.watcher.shard).namespaces(s.watcher.namespaces)
-                  if s.watcher.namespace_scope == "server" and s.watcher.namespaces else [None])
+        self._failure = asyncio.get_running_loop().create_future()
+        scope_mode = s.watcher.namespace_scope
+        if scope_mode == "discover":
+            self.ns_watcher = NamespaceWatcher(self.api, s, self.metrics, self._on_namespaces)
+            ns_task = asyncio.ensure_future(self.ns_watcher.run())
+            self._tasks.append(ns_task)
+            synced = asyncio.ensure_future(self.ns_watcher.synced.wait())
+            await asyncio.wait([synced, ns_task], return_when=asyncio.FIRST_COMPLETED)
+            if not synced.done():
+                synced.cancel()
+                if ns_task.exception() is not None:
+                    raise ns_task.exception()  # type: ignore[misc]
+                raise SetupError("namespace watch ended before the initial list")
+            scopes: List[Optional[str]] = list(self._owned(self.ns_watcher.names))
+        elif scope_mode == "server" and s.watcher.namespaces:
+            scopes = list(ShardFilter(s.watcher.shard).namespaces(s.watcher.namespaces))
+        else:
+            scopes = [None]
+        self._multi = scope_mode == "discover" or len(scopes) > 1
         if s.watcher.shard.count > 1:
             self.log.info(f"Shard {s.watcher.shard.index}/{s.watcher.shard.count} "
                           f"(key={s.watcher.shard.key}); watch scopes: {[x or '*' for x in scopes]}")
@@ -227,40 +254,121 @@ class WatcherService:
             if loaded is not None:
                 saved_rvs, cache, _ = loaded
                 self.log.info(f"Resuming from checkpoint {ck}: {len(cache)} cached pods")
-        self.pipeline = EventPipeline(s, self.decoder, self.notifier, self.metrics, cache, self.event_log)
+        self._saved_rvs = saved_rvs
+        self.pipeline = EventPipeline(s, self.decoder, self.notifier, self.metrics, cache, self.event_log,
+                                      event_sharding=self._event_sharding())
         if self._native_pipeline():
             self._decode_pool = self._make_decode_pool()
             self.pipeline.attach_native(self._decode_pool)
+        if saved_rvs and None not in scopes:
+            # pods of namespaces this shard no longer watches would never be reconciled
+            self._forget_namespaces_except(set(scopes))
         self.metrics.gauges["cached_pods"] = lambda: float(len(cache))
         self.metrics.gauges["notify_outstanding"] = lambda: float(self.notifier.outstanding())
+        self.metrics.gauges["watch_scopes"] = lambda: float(len(self.reflectors))
         self.log.info(f"Starting Pod watcher in {s.environment} environment...")
         if s.watcher.namespaces:
             self.log.info(f"Monitoring namespaces: {s.watcher.namespaces}")
         else:
             self.log.info("Monitoring all namespaces")
         for ns in scopes:
-            key = ns or "*"
-            rv = saved_rvs.get(key)
-            # Each scope decodes its own stream: give it a private decoder.
-            dec = self.decoder if len(scopes) == 1 else make_decoder(
-                s.watcher.engine, s.environment, s.watcher.state_format, s.watcher.payload_extra)
-            pipe = self.pipeline if len(scopes) == 1 else self._scope_pipeline(dec)
-            self.reflectors.append(Reflector(self.api, s, dec, pipe, self.metrics, namespace=ns,
-                                             resource_version=rv, primed=bool(saved_rvs)))
-        for r in self.reflectors:
-            self._tasks.append(asyncio.ensure_future(r.run()))
+            self._start_scope(ns, primed=bool(saved_rvs))
         if s.metrics.enabled and self.serve_metrics:
             self._metrics_server = await start_metrics_server(self.metrics, s.metrics.host, s.metrics.port)
         if ck:
             self._tasks.append(asyncio.ensure_future(self._checkpoint_loop()))
+        self._live = True
+        if self.ns_watcher is not None:
+            self._on_namespaces(self.ns_watcher.names)  # changes seen while the first scopes started
         await self._wait_synced()
         self.metrics.ready = True
         self.started.set()
 
+    # ------------------------------------------------------------------ watch scopes
+    def _event_sharding(self) -> bool:
+        """Per-event shard filtering: off when the watches themselves are the
+        shard's namespaces (server-side scopes keyed by namespace)."""
+        w = self.settings.watcher
+        scoped = w.namespace_scope == "discover" or (w.namespace_scope == "server" and bool(w.namespaces))
+        return not (scoped and w.shard.key == "namespace")
+
+    def _owned(self, names: Set[str]) -> List[str]:
+        return ShardFilter(self.settings.watcher.shard).namespaces(sorted(names))
+
+    def _start_scope(self, ns: Optional[str], primed: bool) -> Reflector:
+        s = self.settings
+        key = ns or "*"
+        if self._multi:
+            # Each scope decodes its own stream: give it a private decoder.
+            dec = make_decoder(s.watcher.engine, s.environment, s.watcher.state_format, s.watcher.payload_extra)
+            pipe = self._scope_pipeline(dec)
+        else:
+            dec, pipe = self.decoder, self.pipeline
+        r = Reflector(self.api, s, dec, pipe, self.metrics, namespace=ns,
+                      resource_version=self._saved_rvs.get(key), primed=primed)
+        if getattr(self.notifier, "saturated", False):
+            r.set_paused(True)
+        self.reflectors.append(r)
+        task = asyncio.ensure_future(r.run())
+        self._scope_tasks[key] = task
+        task.add_done_callback(lambda t, k=key: self._scope_done(k, t))
+        return r
+
+    def _scope_done(self, key: str, task: "asyncio.Task") -> None:
+        if self._scope_tasks.get(key) is not task:
+            return  # stopped on purpose (namespace gone or handed over)
+        if task.cancelled() or self._stop.is_set():
+            return
+        exc = task.exception()
+        if exc is not None and self._failure is not None and not self._failure.done():
+            self._failure.set_exception(exc)
+
+    def _stop_scope(self, ns: str) -> None:
+        task = self._scope_tasks.pop(ns, None)
+        for r in [r for r in self.reflectors if r.namespace == ns]:
+            r.stop()
+            self.reflectors.remove(r)
+        if task is not None and not task.done():
+            task.cancel()
+        self._forget_namespaces({ns})
+
+    def _forget_namespaces(self, namespaces: Set[str]) -> None:
+        """Drop cached pods of namespaces this shard stopped watching, silently:
+        they are now the business of another shard (or gone with the namespace)."""
+        cache = self.pipeline.cache if self.pipeline is not None else None
+        if cache is None:
+            return
+        for uid, ent in cache.items():
+            if ent[2] in namespaces:
+                cache.pop(uid, None)
+
+    def _forget_namespaces_except(self, keep: Set[str]) -> None:
+        cache = self.pipeline.cache if self.pipeline is not None else None
+        if cache is None:
+            return
+        for uid, ent in cache.items():
+            if ent[2] not in keep:
+                cache.pop(uid, None)
+
+    def _on_namespaces(self, names: Set[str]) -> None:
+        """NamespaceWatcher callback: start/stop reflectors to match the owned set."""
+        if not self._live or self._stop.is_set():
+            return
+        owned = set(self._owned(names))
+        current = set(self._scope_tasks)
+        for ns in sorted(owned - current):
+            self.metrics.c["scopes_started"] += 1
+            self.log.info(f"Watching namespace {ns} (new or now owned by shard {self.settings.watcher.shard.index})")
+            self._start_scope(ns, primed=True)
+        for ns in sorted(current - owned):
+            self.metrics.c["scopes_stopped"] += 1
+            self.log.info(f"Stopped watching namespace {ns} (deleted or owned by another shard)")
+            self._stop_scope(ns)
+
     def _scope_pipeline(self, decoder) -> EventPipeline:
         assert self.pipeline is not None
         p = EventPipeline(self.settings, decoder, self.notifier, self.metrics, self.pipeline.cache,
-                          self.event_log)
+                          self.event_log, event_sharding=self._event_sharding())
         if self._native_pipeline():
             p.attach_native(self._decode_pool)
         return p
@@ -288,23 +396,27 @@ class WatcherService:
 
     async def _wait_synced(self) -> None:
         synced = asyncio.ensure_future(asyncio.gather(*[r.synced.wait() for r in self.reflectors]))
-        runs = list(self._tasks)
+        runs = list(self._tasks) + list(self._scope_tasks.values())
         done, _ = await asyncio.wait([synced] + runs, return_when=asyncio.FIRST_COMPLETED)
         if synced not in done:
             synced.cancel()
             for t in runs:
-                if t.done() and t.exception() is not None:
+                if t.done() and not t.cancelled() and t.exception() is not None:
                     raise t.exception()  # type: ignore[misc]
             raise SetupError("watch ended before the initial sync")
 
     async def wait(self) -> None:
-        """Run until :meth:`stop` or a reflector fails permanently."""
+        """Run until :meth:`stop` or a watch fails permanently."""
         stopper = asyncio.ensure_future(self._stop.wait())
-        tasks = [t for t in self._tasks] + [stopper]
-        done, _ = await asyncio.wait(tasks, return_when=asyncio.FIRST_COMPLETED)
+        waits = [t for t in self._tasks] + [stopper]
+        if self._failure is not None:
+            waits.append(self._failure)
+        if not self._multi:
+            waits += list(self._scope_tasks.values())  # a lone watch that ends ends the service
+        done, _ = await asyncio.wait(waits, return_when=asyncio.FIRST_COMPLETED)
         err = None
         for t in done:
-            if t is not stopper and t.exception() is not None:
+            if t is not stopper and not t.cancelled() and t.exception() is not None:
                 err = t.exception()
         if not stopper.done():
             stopper.cancel()
@@ -313,6 +425,8 @@ class WatcherService:
 
     def stop(self) -> None:
         self._stop.set()
+        if self.ns_watcher is not None:
+            self.ns_watcher.stop()
         for r in self.reflectors:
             r.stop()
 
@@ -333,6 +447,8 @@ class WatcherService:
         overwrite newer state.
         """
         self.log.info("Stopping Pod watcher...")
+        if self.ns_watcher is not None:
+            self.ns_watcher.stop()
         for r in self.reflectors:
             r.stop()
         drained = True
@@ -346,10 +462,11 @@ class WatcherService:
                 closed = drained = True
         if checkpoint and drained:
             await self._write_checkpoint()
-        for t in self._tasks:
+        tasks = list(self._tasks) + list(self._scope_tasks.values())
+        for t in tasks:
             if not t.done():
                 t.cancel()
-        for t in self._tasks:
+        for t in tasks:
             try:
                 await t
             except (asyncio.CancelledError, WatchFailed, Exception):  # noqa: BLE001

@@ -131,6 +131,23 @@ class KubeApi:
             raise ApiError(stream.status, stream.reason, err, stream.headers)
         return stream
 
+    async def watch_namespaces(self, sink: Callable[[bytes, int], None],
+                               resource_version: Optional[str] = None,
+                               timeout_seconds: Optional[int] = None,
+                               connect_timeout: Optional[float] = None) -> StreamResponse:
+        """``GET /api/v1/namespaces?watch=true`` (namespace discovery for
+        ``watcher.namespace_scope: discover``); de-chunked NDJSON to ``sink``."""
+        q: Dict[str, object] = {"watch": "true", "allowWatchBookmarks": "true"}
+        if resource_version:
+            q["resourceVersion"] = resource_version
+        if timeout_seconds:
+            q["timeoutSeconds"] = int(timeout_seconds)
+        stream, err = await self.http.stream("GET", "/api/v1/namespaces", sink, query=q,
+                                             timeout=connect_timeout)
+        if err is not None:
+            raise ApiError(stream.status, stream.reason, err, stream.headers)
+        return stream
+
     # ------------------------------------------------------------------ coordination.k8s.io/v1
     # Lease objects back leader election (engine/leader.py); the reference runs
     # a single replica and has no equivalent.

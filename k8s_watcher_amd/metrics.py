@@ -50,6 +50,9 @@ COUNTERS = (
     "expired_410",
     "expired_relist_backoffs",  # 410s right after a relist (no progress): the next relist waited
     "checkpoints_written",
+    "namespace_changes",    # namespace set changes seen by watcher.namespace_scope: discover
+    "scopes_started",       # per-namespace pod watches opened after start-up (new or handed-over namespaces)
+    "scopes_stopped",       # ... and closed (namespace deleted or now owned by another shard)
     "leader_acquired",      # leadership terms started (engine/leader.py)
     "leader_lost",
     "lease_update_conflicts",

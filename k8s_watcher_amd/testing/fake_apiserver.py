@@ -162,7 +162,10 @@ class FakeApiServer:
         self.lease_writes: List[Tuple[Tuple[str, str], Dict[str, Any]]] = []
         self.lease_fault: Optional[int] = None  # answer every lease request with this status
         self.lease_stall = 0.0  # seconds every lease request waits before it is answered
-        self.expire_every_watch = False  # a lagging watch cache: every watch with an RV gets 410
+        self.expire_every_watch = False
+        self.deleted_namespaces: Set[str] = set()
+        self.ns_watches: Set[asyncio.StreamWriter] = set()
+        self._known_ns: Set[str] = set(self.extra_namespaces)  # a lagging watch cache: every watch with an RV gets 410
 
     # ------------------------------------------------------------------ lifecycle
     async def start(self, host: str = "127.0.0.1", port: int = 0, ssl_context=None) -> int:
@@ -217,10 +220,48 @@ class FakeApiServer:
                 except Exception:  # noqa: BLE001
                     self.watches.discard(w)
 
+    # ------------------------------------------------------------------ namespaces
+    def namespace_names(self) -> List[str]:
+        return sorted(({ns for ns, _ in self.pods} | set(self.extra_namespaces)) - self.deleted_namespaces)
+
+    def _ns_event(self, etype: str, name: str) -> None:
+        obj = {"kind": "Namespace", "apiVersion": "v1",
+               "metadata": {"name": name, "uid": str(uuid.uuid5(uuid.NAMESPACE_DNS, name)),
+                            "resourceVersion": str(self._next_rv())},
+               "status": {"phase": "Active"}}
+        data = _chunk(json.dumps({"type": etype, "object": obj}, separators=(",", ":")).encode() + b"\n")
+        for w in list(self.ns_watches):
+            try:
+                w.write(data)
+            except Exception:  # noqa: BLE001
+                self.ns_watches.discard(w)
+
+    def _touch_namespace(self, name: str) -> None:
+        if name not in self._known_ns or name in self.deleted_namespaces:
+            self._known_ns.add(name)
+            self.deleted_namespaces.discard(name)
+            self._ns_event("ADDED", name)
+
+    def add_namespace(self, name: str) -> None:
+        if name not in self.extra_namespaces:
+            self.extra_namespaces.append(name)
+        self._touch_namespace(name)
+
+    def delete_namespace(self, name: str) -> None:
+        """Delete every pod in ``name`` (DELETED events), then the namespace itself."""
+        for (ns, pname) in [k for k in self.pods if k[0] == name]:
+            self.delete(ns, pname)
+        if name in self.extra_namespaces:
+            self.extra_namespaces.remove(name)
+        self.deleted_namespaces.add(name)
+        self._known_ns.discard(name)
+        self._ns_event("DELETED", name)
+
     def create(self, pod: Dict[str, Any]) -> Dict[str, Any]:
         pod = copy.deepcopy(pod)
         md = pod.setdefault("metadata", {})
         md.setdefault("namespace", "default")
+        self._touch_namespace(md["namespace"])
         md.setdefault("uid", str(uuid.uuid4()))
         md.setdefault("creationTimestamp", time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()))
         md["resourceVersion"] = str(self._next_rv())
@@ -341,7 +382,7 @@ class FakeApiServer:
                     return
                 method, target = parts[0], parts[1]
                 self.requests.append((method, target))
-                keep = await self._route(method, target, headers, writer, body)
+                keep = await self._route(method, target, headers, writer, body, reader)
                 if not keep:
                     return
         except (ConnectionError, asyncio.IncompleteReadError):
@@ -365,7 +406,7 @@ class FakeApiServer:
                      % (code, reason.encode(), extra, len(body)) + body)
 
     async def _route(self, method: str, target: str, headers: Dict[str, str], writer,
-                     body: bytes = b"") -> bool:
+                     body: bytes = b"", reader: Optional[asyncio.StreamReader] = None) -> bool:
         u = urlsplit(target)
         q = {k: v[-1] for k, v in parse_qs(u.query, keep_blank_values=True).items()}
         path = u.path
@@ -406,8 +447,26 @@ class FakeApiServer:
             self._send_json(writer, 200, {"major": "1", "minor": "33", "gitVersion": "v1.33.1-fake",
                                           "platform": "linux/amd64"})
             return True
+        if path == "/api/v1/namespaces" and q.get("watch") in ("true", "1"):
+            writer.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\n"
+                         b"Transfer-Encoding: chunked\r\n\r\n")
+            self.ns_watches.add(writer)
+            try:
+                await writer.drain()
+                timeout = float(q.get("timeoutSeconds") or 3600)
+                try:  # until the client goes away or the server-side timeout
+                    await with_timeout(reader.read() if reader is not None else writer.wait_closed(), timeout)
+                except (asyncio.TimeoutError, ConnectionError):
+                    pass
+                try:
+                    writer.write(b"0\r\n\r\n")
+                except Exception:  # noqa: BLE001
+                    pass
+            finally:
+                self.ns_watches.discard(writer)
+            return False
         if path == "/api/v1/namespaces":
-            names = sorted({ns for ns, _ in self.pods} | set(self.extra_namespaces))
+            names = self.namespace_names()
             items = [{"kind": "Namespace", "apiVersion": "v1",
                       "metadata": {"name": n, "uid": str(uuid.uuid5(uuid.NAMESPACE_DNS, n))},
                       "status": {"phase": "Active"}} for n in names]

@@ -281,7 +281,7 @@ class WatcherSettings:
     log_level: str = "INFO"
     log_file: Optional[str] = None
     namespaces: List[str] = field(default_factory=list)
-    namespace_scope: str = "client"  # client | server
+    namespace_scope: str = "client"  # client | server | discover
     label_selector: Optional[str] = None
     field_selector: Optional[str] = None
     critical_events_only: bool = False
@@ -314,6 +314,7 @@ class ShardSettings:
     count: int = 1
     index: int = 0
     key: str = "namespace"  # namespace | uid
+    assignment: str = "hash"  # hash | balanced: namespace -> shard for per-namespace watches (parallel/shard.py)
 
 
 @dataclass
@@ -349,7 +350,9 @@ def _shard(block: Dict[str, Any]) -> ShardSettings:
     count = os.environ.get("K8S_WATCHER_SHARD_COUNT", block.get("count", 1))
     index = os.environ.get("K8S_WATCHER_SHARD_INDEX", block.get("index", 0))
     s = ShardSettings(count=_as_int(count, "watcher.shard.count"), index=_as_int(index, "watcher.shard.index"),
-                      key=_choice(block.get("key", "namespace"), "watcher.shard.key", ("namespace", "uid")))
+                      key=_choice(block.get("key", "namespace"), "watcher.shard.key", ("namespace", "uid")),
+                      assignment=_choice(block.get("assignment", "hash"), "watcher.shard.assignment",
+                                         ("balanced", "hash")))
     if s.count < 1 or not 0 <= s.index < s.count:
         raise ConfigError(f"watcher.shard: index {s.index} outside [0, {s.count})")
     return s
@@ -439,7 +442,8 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         log_level=level,
         log_file=w.get("log_file") or None,
         namespaces=list(namespaces),
-        namespace_scope=_choice(w.get("namespace_scope", "client"), "watcher.namespace_scope", ("client", "server")),
+        namespace_scope=_choice(w.get("namespace_scope", "client"), "watcher.namespace_scope",
+                                ("client", "server", "discover")),
         label_selector=w.get("label_selector") or None,
         field_selector=w.get("field_selector") or None,
         critical_events_only=_as_bool(alerts.get("critical_events_only", False), "watcher.alerts.critical_events_only"),

@@ -121,3 +121,103 @@ def test_bench_two_ranks_gloo():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * 1500
     assert d["value"] > 0 and d["scaling"] == "weak"
+
+
+def test_balanced_assignment_bounded_and_stable():
+    from k8s_watcher_amd.parallel.shard import balanced_assignment
+    names = [f"tenant-{i:03d}" for i in range(67)]
+    for n in (1, 2, 3, 4, 8, 16):
+        a = balanced_assignment(names, n)
+        assert set(a) == set(names)
+        loads = collections.Counter(a.values())
+        assert max(loads.values()) <= -(-len(names) // n)
+        assert balanced_assignment(list(reversed(names)), n) == a  # order-independent
+        owned = [ShardFilter(ShardSettings(n, i)).namespaces(names) for i in range(n)]
+        assert sorted(sum(owned, [])) == sorted(names)  # total and disjoint
+    # removing one namespace never moves the others
+    a = balanced_assignment(names, 8)
+    b = balanced_assignment(names[1:], 8)
+    assert sum(a[x] != b[x] for x in names[1:]) <= 8
+
+
+@pytest.mark.parametrize("assignment", ["hash", "balanced"])
+def test_discover_scope_two_shards_exactly_once(assignment):
+    """namespace_scope: discover — two shard processes (here: two services on
+    one loop) watch only the namespaces they own, follow namespaces that are
+    created and deleted, and together deliver every event exactly once. With
+    ``balanced`` a new namespace can move others to the other shard: their
+    pods are then re-announced as ADDED by the new owner (and only those)."""
+    import asyncio
+
+    from conftest import run
+    from k8s_watcher_amd.engine.service import WatcherService
+    from k8s_watcher_amd.kube.kubeconfig import KubeEndpoint
+    from k8s_watcher_amd.metrics import Metrics
+
+    async def body():
+        nss = [f"ns-{i}" for i in range(10)]
+        srv = FakeApiServer(namespaces=nss)
+        await srv.start()
+        sink = StubSink()
+        await sink.start()
+        svcs = []
+        for i in range(2):
+            s = load_settings("staging", overrides={
+                "clusterapi": {"base_url": sink.url, "health_check_on_start": False},
+                "watcher": {"namespace_scope": "discover",
+                            "shard": {"count": 2, "index": i, "assignment": assignment},
+                            "retry": {"delay_seconds": 0.05, "max_attempts": 0}}})
+            svc = WatcherService(s, endpoint=KubeEndpoint(server=srv.url), metrics=Metrics())
+            await svc.start()
+            svcs.append(svc)
+        owned = [sorted(r.namespace for r in svc.reflectors) for svc in svcs]
+        assert sorted(owned[0] + owned[1]) == sorted(nss)
+        if assignment == "balanced":
+            assert len(owned[0]) == len(owned[1]) == 5
+        f = PodFactory(seed=5, namespaces=nss)
+        created = [srv.create(f.new_pod()) for _ in range(40)]
+        uids = [p["metadata"]["uid"] for p in created]
+        srv_ns = {p["metadata"]["uid"]: p["metadata"]["namespace"] for p in created}
+        await sink.state.wait_for(40, timeout=10)
+        # a new namespace appears: exactly one shard starts watching it
+        srv.add_namespace("late-ns")
+        for _ in range(50):
+            if sum(any(r.namespace == "late-ns" for r in svc.reflectors) for svc in svcs) == 1:
+                break
+            await asyncio.sleep(0.05)
+        late = [srv.create(f.new_pod(namespace="late-ns"))["metadata"]["uid"] for _ in range(3)]
+        await sink.state.wait_for(43, timeout=10)
+        await asyncio.sleep(0.2)
+        # a namespace is deleted: its pods go DELETED, then its watch stops
+        gone = owned[0][0]
+        doomed = [p["metadata"]["uid"] for (ns, _), p in srv.pods.items() if ns == gone]
+        srv.delete_namespace(gone)
+        await sink.state.wait_for(43 + len(doomed), timeout=10)
+        for _ in range(50):
+            if not any(r.namespace == gone for r in svcs[0].reflectors):
+                break
+            await asyncio.sleep(0.05)
+        assert not any(r.namespace == gone for svc in svcs for r in svc.reflectors)
+        await asyncio.sleep(0.2)
+        got = collections.Counter((p["uid"], p["event_type"]) for p in sink.state.payloads())
+        want = collections.Counter([(u, "ADDED") for u in uids + late] + [(u, "DELETED") for u in doomed])
+        if assignment == "hash":
+            assert got == want
+        else:
+            moved = {ns for ns in nss if ns != gone
+                     and any(r.namespace == ns for r in svcs[0].reflectors) != (ns in owned[0])}
+            extra = got - want
+            assert not (want - got)  # nothing lost
+            assert all(t == "ADDED" and srv_ns[u] in moved for (u, t) in extra), (extra, moved)
+        # each shard only ever opened pod watches for namespaces it owned
+        for svc, mine in zip(svcs, owned):
+            assert svc.metrics.c["events_other_shard"] == 0
+        watch_paths = [t.split("?")[0] for _, t in srv.requests if "watch=true" in t and "/pods" in t]
+        assert all(p.startswith("/api/v1/namespaces/") for p in watch_paths)
+        for svc in svcs:
+            svc.stop()
+            await svc.shutdown()
+        await sink.stop()
+        await srv.stop()
+
+    run(body(), timeout=60)
