@@ -6,24 +6,38 @@ BASELINE.json metric: "pod-events/sec sustained + p50 event→notify latency
 all-namespaces watch, 10k-pod churn, async HTTP notifier pool. The reference
 publishes no numbers, so the reference-equivalent pipeline
 (``benchmarks/reference_equiv.py``) is measured on the same replay in the same
-run and ``vs_baseline`` is the ratio to it.
+run and ``vs_baseline`` is the ratio to it (a model of the reference: parity
+unpinned).
 
-Per rank (one watcher process per rank; ``torchrun`` ranks = independent
-namespace shards, weak scaling):
+One cluster, N watcher shards (``torchrun`` ranks = the product's sharded
+scale-out, weak scaling):
 
-* a replay API server child (``testing/replay_server.py``) streams one *step* =
-  ``--pods-per-step`` pod lifecycles (ADDED → 3×MODIFIED → DELETED, ≈4 KB of
-  real-shaped Pod JSON per event, one HTTP chunk per event);
-* a stub clusterapi child (``testing/stub_sink.py``) acks every POST;
-* this process runs the real :class:`WatcherService` (production profile:
-  critical-events filter, namespace filter, notifier pool) and a step ends when
-  every event of the step has been decoded, filtered and — if it survived the
-  filters — POSTed and acknowledged (2xx) by the sink.
+* rank 0 starts ONE API-server fixture for everyone
+  (``testing/cluster_replay.py``: ``--pods-per-step × N`` pod lifecycles per
+  step — ADDED → 3×MODIFIED → DELETED, ≈4 KB of real-shaped Pod JSON per
+  event — over ``--namespaces`` namespaces, one global resourceVersion
+  sequence, served by several SO_REUSEPORT worker processes) and ONE stub
+  clusterapi (``testing/stub_sink.py``, SO_REUSEPORT workers, verify mode:
+  it counts every ``uid|event_type|phase`` it acknowledges);
+* every rank runs the real :class:`WatcherService` with the production
+  profile (critical-events filter, namespace filter over ``--targets`` —
+  half the namespaces — WARNING log, async notifier pool) as shard
+  ``rank`` of ``N``: with N > 1, ``watcher.namespace_scope: discover`` — it
+  watches the namespace list and opens pod watches only for the namespaces
+  it owns (``shard.assignment: balanced``), so the API server sends each event
+  to exactly one shard. With N = 1 the watcher makes the reference's single
+  cluster-wide watch (``--watch-scope`` overrides either);
+* a step ends on a rank when every event of its namespaces in that step has
+  been decoded, filtered and — if it survived the filters — POSTed and
+  acknowledged (2xx) by clusterapi; ranks meet at a barrier after each step.
 
 ``W`` warmup steps run untimed, then exactly ``K`` steps are timed between
-barriers; the slowest rank's time is used. Latency (socket read of the watch
-chunk → 2xx from clusterapi) is measured afterwards at the config's nominal
-rate (``--latency-rate``, default 100 ev/s as in config #4).
+barriers; the slowest rank's clock is used and ``value`` is the events of all
+ranks over it. Then the latency phase paces ``--latency-rate`` ev/s per rank
+(config #4's 100 ev/s) for ``--latency-seconds``: p50/p99 of socket read of the
+watch chunk → 2xx from clusterapi, over the samples of every rank. Last, the
+sink's counts prove the union of the shards delivered every notifiable event
+exactly once (``verify``: no event missing, none twice, none by two shards).
 
 Usage: ``python bench.py [--gpus N] [--steps K] [--warmup W]`` (one JSON line on
 rank 0). There is no device work in this workload — see SURVEY.md §2.2 — so
@@ -35,11 +49,14 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import glob
 import json
 import os
+import shutil
 import signal
 import socket
 import sys
+import tempfile
 import threading
 import time
 
@@ -51,10 +68,17 @@ METRIC = "pod-events/sec sustained + p50 event→notify latency (single process,
 
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--gpus", type=int, default=1, help="ranks (one watcher process each)")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one watcher shard process each)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pods-per-step", type=int, default=10000, help="pod lifecycles per step (5 events each)")
+    ap.add_argument("--pods-per-step", type=int, default=10000,
+                    help="pod lifecycles per step PER RANK (5 events each; the cluster has N times as many)")
+    ap.add_argument("--namespaces", type=int, default=64, help="namespaces in the cluster")
+    ap.add_argument("--targets", default="even",
+                    help="watcher.namespaces: 'even' (every other namespace), 'all', or a comma list")
+    ap.add_argument("--watch-scope", default="auto", choices=["auto", "cluster", "discover"],
+                    help="auto: one cluster-wide watch for N=1, per-namespace shard watches for N>1")
+    ap.add_argument("--assignment", default="balanced", choices=["balanced", "hash"])
     ap.add_argument("--profile", default="production", choices=["development", "staging", "production"])
     ap.add_argument("--engine", default="native", choices=["native", "python"])
     ap.add_argument("--connections", type=int, default=None, help="notifier pool connections")
@@ -69,9 +93,12 @@ def parse_args(argv=None):
                     help="serve the C++ notifier core's sockets on its own thread (clusterapi.pool.io_thread)")
     ap.add_argument("--tls", action="store_true",
                     help="https clusterapi (as production.yaml): the stub sink serves TLS with a throw-away CA")
-    ap.add_argument("--sink-workers", type=int, default=4)
-    ap.add_argument("--latency-rate", type=float, default=100.0)
-    ap.add_argument("--latency-seconds", type=float, default=3.0)
+    ap.add_argument("--sink-workers", type=int, default=None, help="default 4 per rank")
+    ap.add_argument("--fixture-workers", type=int, default=None, help="default 2 per rank")
+    ap.add_argument("--no-verify", dest="verify", action="store_false",
+                    help="sink does not count payload keys (no exactly-once proof)")
+    ap.add_argument("--latency-rate", type=float, default=100.0, help="ev/s per rank in the latency phase")
+    ap.add_argument("--latency-seconds", type=float, default=30.0)
     ap.add_argument("--ref-events", type=int, default=10000,
                     help="events for the reference-equivalent run (0 = skip, vs_baseline null)")
     ap.add_argument("--step-timeout", type=float, default=300.0)
@@ -92,15 +119,26 @@ class Dist:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank)))
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
-        self.pg = None
         if self.world > 1:
+            import datetime
+
             import torch.distributed as dist
-            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world,
+                                    timeout=datetime.timedelta(minutes=30))
             self.dist = dist
 
     def barrier(self) -> None:
         if self.world > 1:
             self.dist.barrier()
+
+    async def abarrier(self) -> None:
+        """Barrier that keeps this rank's event loop (its watcher) running."""
+        if self.world == 1:
+            return
+        work = self.dist.barrier(async_op=True)
+        while not work.is_completed():
+            await asyncio.sleep(0.0002)
+        work.wait()
 
     def all_gather(self, obj) -> list:
         if self.world == 1:
@@ -108,6 +146,13 @@ class Dist:
         out = [None] * self.world
         self.dist.all_gather_object(out, obj)
         return out
+
+    def broadcast(self, obj):
+        if self.world == 1:
+            return obj
+        box = [obj]
+        self.dist.broadcast_object_list(box, src=0)
+        return box[0]
 
     def reduce(self, value: float, op: str) -> float:
         if self.world == 1:
@@ -159,49 +204,138 @@ def placement(d: "Dist"):
     return set(doms[assign_domains(wanted, doms)[d.rank]])
 
 
+def target_namespaces(spec: str, names):
+    if spec == "all":
+        return list(names)
+    if spec == "even":
+        return [n for i, n in enumerate(names) if i % 2 == 0]
+    return [x for x in spec.split(",") if x]
+
+
+class Fixtures:
+    """Rank 0's cluster fixture + stub clusterapi (shared by every rank)."""
+
+    def __init__(self) -> None:
+        self.replay = None
+        self.sink = None
+        self.info: dict = {}
+        self.verify_dir = None
+        self.pki = None
+
+    async def start(self, args, world: int, names, targets) -> dict:
+        fw = args.fixture_workers or max(2, 2 * world)
+        self.replay = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.cluster_replay",
+                                  "--pods", str(args.pods_per_step * world),
+                                  "--namespace-list", ",".join(names), "--targets", ",".join(targets),
+                                  "--workers", str(fw))
+        sink_port = free_port()
+        tls_args = []
+        if args.tls:
+            from k8s_watcher_amd.testing.certs import make_pki
+            self.pki = make_pki(tempfile.mkdtemp(prefix="bench-pki-"))
+            tls_args = ["--tls-cert", self.pki.server_crt, "--tls-key", self.pki.server_key]
+        self.sink_workers = args.sink_workers or 4 * world
+        verify = []
+        if args.verify:
+            self.verify_dir = tempfile.mkdtemp(prefix="bench-verify-")
+            verify = ["--verify-dir", self.verify_dir]
+        self.sink = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.stub_sink", "--port", str(sink_port),
+                                "--workers", str(self.sink_workers), *tls_args, *verify)
+        line = (await asyncio.wait_for(self.replay.stdout.readline(), 600)).decode()
+        assert line.startswith("READY "), line
+        self.info = json.loads(line[6:])
+        await asyncio.wait_for(self.sink.stdout.readline(), 60)
+        await asyncio.sleep(0.3)  # let every SO_REUSEPORT worker bind
+        scheme = "https" if args.tls else "http"
+        return {"api_port": self.info["port"], "sink_url": f"{scheme}://127.0.0.1:{sink_port}",
+                "ns_events": self.info["namespaces"], "events_per_step": self.info["events_per_step"],
+                "notifiable_per_step": self.info["notifiable_per_step"],
+                "ca": self.pki.ca_crt if self.pki else None, "fixture_workers": self.info["workers"]}
+
+    async def cmd(self, line: str) -> list:
+        self.replay.stdin.write((line + "\n").encode())
+        await self.replay.stdin.drain()
+        return (await self.replay.stdout.readline()).decode().split()
+
+    async def verify_counts(self) -> dict:
+        """Snapshot of the sink's key counts over all its workers (SIGUSR1)."""
+        for f in glob.glob(os.path.join(self.verify_dir, "sink-*.json")):
+            os.unlink(f)
+        os.killpg(self.sink.pid, signal.SIGUSR1)
+        deadline = time.monotonic() + 60
+        files = []
+        while time.monotonic() < deadline:
+            files = glob.glob(os.path.join(self.verify_dir, "sink-*.json"))
+            if len(files) >= self.sink_workers:
+                break
+            await asyncio.sleep(0.05)
+        keys: dict = {}
+        total = 0
+        for f in files:
+            with open(f) as fh:
+                doc = json.load(fh)
+            total += doc["count"]
+            for k, v in doc["keys"].items():
+                keys[k] = keys.get(k, 0) + v
+        return {"workers_reporting": len(files), "received": total, "unique": len(keys),
+                "duplicates": sum(v - 1 for v in keys.values() if v > 1)}
+
+    async def close(self) -> None:
+        if self.replay is not None and self.replay.returncode is None:
+            try:
+                self.replay.stdin.write(b"QUIT\n")
+                await self.replay.stdin.drain()
+            except (ConnectionError, RuntimeError):
+                pass
+        for p in (self.replay, self.sink):
+            if p is None:
+                continue
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except (ProcessLookupError, PermissionError):
+                pass
+            try:
+                await asyncio.wait_for(p.wait(), 5)
+            except asyncio.TimeoutError:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+            transport = getattr(p, "_transport", None)
+            if transport is not None:
+                transport.close()  # close pipes while the loop is alive (no __del__ noise)
+        if self.verify_dir:
+            shutil.rmtree(self.verify_dir, ignore_errors=True)
+
+
 async def rank_main(args, d: Dist) -> dict:
     from k8s_watcher_amd.engine.service import WatcherService
     from k8s_watcher_amd.kube.kubeconfig import KubeEndpoint
     from k8s_watcher_amd.metrics import Metrics
+    from k8s_watcher_amd.testing.cluster_replay import namespace_names
     from k8s_watcher_amd.utils.config import load_settings
     from k8s_watcher_amd.utils.logsetup import setup_logging
 
+    scope = args.watch_scope if args.watch_scope != "auto" else ("cluster" if d.world == 1 else "discover")
+    names = namespace_names(args.namespaces)
+    targets = target_namespaces(args.targets, names)
     watcher_cpus = placement(d) if args.placement else None
     if watcher_cpus:
         os.sched_setaffinity(0, watcher_cpus)  # the decode workers inherit it
-    replay = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.replay_server",
-                         "--pods-per-step", str(args.pods_per_step), "--seed", str(d.rank),
-                         "--prerender", str(args.warmup + args.steps))
-    sink_port = free_port()
-    tls_args, pki = [], None
-    if args.tls:
-        import tempfile
-        from k8s_watcher_amd.testing.certs import make_pki
-        pki = make_pki(tempfile.mkdtemp(prefix="bench-pki-"))
-        tls_args = ["--tls-cert", pki.server_crt, "--tls-key", pki.server_key]
-    scheme = "https" if args.tls else "http"
-    sink = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.stub_sink", "--port", str(sink_port),
-                       "--workers", str(args.sink_workers), *tls_args)
+    fx = Fixtures()
     try:
-        ready = (await asyncio.wait_for(replay.stdout.readline(), 600)).decode().split()
-        assert ready and ready[0] == "READY", ready
-        api_port, events_per_step = int(ready[1]), int(ready[2])
-        await asyncio.wait_for(sink.stdout.readline(), 60)
-        await asyncio.sleep(0.3)  # let every SO_REUSEPORT worker bind
-
-        async def cmd(line: str) -> int:
-            replay.stdin.write((line + "\n").encode())
-            await replay.stdin.drain()
-            reply = (await replay.stdout.readline()).decode().split()
-            return int(reply[2])
-
+        shared = await fx.start(args, d.world, names, targets) if d.rank == 0 else None
+        shared = d.broadcast(shared)
         log_path = os.path.join("/tmp", f"k8s-watcher-bench-{os.getpid()}.log")
         setup_logging(args.profile, "WARNING" if args.profile == "production" else "INFO", log_file=log_path)
         overrides = {
-            "clusterapi": {"base_url": f"{scheme}://127.0.0.1:{sink_port}", "timeout": 30,
-                           **({"ca_file": pki.ca_crt} if pki else {}),
+            "clusterapi": {"base_url": shared["sink_url"], "timeout": 30,
+                           **({"ca_file": shared["ca"]} if shared["ca"] else {}),
                            "enabled": not os.environ.get("BENCH_NO_NOTIFY")},
             "watcher": {"engine": args.engine, "retry": {"max_attempts": 0, "delay_seconds": 0.05},
+                        "namespaces": targets,
+                        "namespace_scope": "discover" if scope == "discover" else "client",
+                        "shard": {"count": d.world, "index": d.rank, "assignment": args.assignment},
                         **({"decode_threads": args.decode_threads} if args.decode_threads is not None else {}),
                         **({"watch_read_bytes": args.watch_read_bytes} if args.watch_read_bytes else {}),
                         # placement already pinned this thread (the decode workers inherit it)
@@ -222,108 +356,127 @@ async def rank_main(args, d: Dist) -> dict:
         if settings.watcher.log_level:
             setup_logging(args.profile, settings.watcher.log_level, log_file=log_path)
         metrics = Metrics(record_samples=True)
-        svc = WatcherService(settings, endpoint=KubeEndpoint(server=f"http://127.0.0.1:{api_port}"),
+        svc = WatcherService(settings, endpoint=KubeEndpoint(server=f"http://127.0.0.1:{shared['api_port']}"),
                              metrics=metrics)
         await svc.start()
-        for _ in range(200):
-            if await cmd("WATCHERS 0") >= 1:
-                break
-            await asyncio.sleep(0.01)
+        mine = sorted(r.namespace for r in svc.reflectors if r.namespace) if scope == "discover" else ["*"]
+        per_step = (shared["events_per_step"] if mine == ["*"]
+                    else sum(shared["ns_events"][ns] for ns in mine))
+        streams = sum(d.all_gather(len(svc.reflectors)))
+        if d.rank == 0:
+            for _ in range(2000):
+                if int((await fx.cmd("WATCHERS"))[2]) >= streams:
+                    break
+                await asyncio.sleep(0.01)
+            await fx.cmd("PREPARE 0 2")
+        d.barrier()
 
         c = metrics.c
         native_pl = svc.pipeline.native if svc.pipeline is not None else None
         decode_threads = native_pl.decode_threads() if native_pl is not None else None
-
         debug = bool(os.environ.get("BENCH_DEBUG"))
+        notifiable = [0]
 
-        async def run_step(k: int, pace: str = "") -> None:
+        async def run_step(k: int, expect: int, pace: str = "") -> None:
             base = c["events_received"]
             t_start = time.perf_counter()
-            n = await cmd(f"PACE {k} {pace}" if pace else f"STEP {k}")
-            t_sent = time.perf_counter()
-            t_ingest = None
+            sent = asyncio.ensure_future(fx.cmd(f"PACE {k} {pace}" if pace else f"STEP {k}")) \
+                if d.rank == 0 else None
             deadline = time.monotonic() + args.step_timeout
-            while c["events_received"] < base + n or svc.notifier.outstanding() > 0:
-                if t_ingest is None and c["events_received"] >= base + n:
-                    t_ingest = time.perf_counter()
+            while c["events_received"] < base + expect or svc.notifier.outstanding() > 0:
                 if time.monotonic() > deadline:
-                    raise TimeoutError(f"step {k}: {c['events_received'] - base}/{n} events, "
+                    raise TimeoutError(f"rank {d.rank} step {k}: {c['events_received'] - base}/{expect} events, "
                                        f"{svc.notifier.outstanding()} notifications outstanding")
                 await asyncio.sleep(0.0005)
+            if sent is not None:
+                notifiable[0] += int((await sent)[3])
             if debug:
-                t_end = time.perf_counter()
-                print(f"step {k}: sent {t_sent - t_start:.3f}s ingest "
-                      f"{(t_ingest or t_end) - t_start:.3f}s done {t_end - t_start:.3f}s", file=sys.stderr)
+                print(f"rank {d.rank} step {k}: {time.perf_counter() - t_start:.3f}s", file=sys.stderr)
+            await d.abarrier()
 
         for k in range(args.warmup):
-            await run_step(k)
+            await run_step(k, per_step)
         metrics.latency.reset()
         d.barrier()
         n0, s0 = c["events_received"], c["notify_delivered"]
-        cpu0 = cpu_snapshot(replay.pid, sink.pid)
+        cpu0 = cpu_snapshot(fx)
         t0 = time.perf_counter()
         for k in range(args.warmup, args.warmup + args.steps):
-            await run_step(k)
+            await run_step(k, per_step)
         elapsed = time.perf_counter() - t0
-        cpu1 = cpu_snapshot(replay.pid, sink.pid)
-        d.barrier()
+        cpu1 = cpu_snapshot(fx)
         events = c["events_received"] - n0
         notified = c["notify_delivered"] - s0
-        sat_p50 = metrics.latency.percentile_ns(50)
+        sat = list(metrics.latency.samples or [])
 
-        # latency at the nominal rate (untimed)
+        # latency at the nominal rate, per rank (untimed)
         metrics.latency.reset()
-        count = max(1, int(args.latency_rate * args.latency_seconds))
-        await run_step(args.warmup + args.steps, f"{args.latency_rate} {count}")
-        p50 = metrics.latency.percentile_ns(50)
-        p99 = metrics.latency.percentile_ns(99)
-        lat_n = metrics.latency.n
+        k_lat = args.warmup + args.steps
+        count = max(1, int(args.latency_rate * d.world * args.latency_seconds))
+        count = min(count, shared["events_per_step"])
+        await run_latency(fx, d, svc, c, k_lat, args.latency_rate * d.world, count, args.step_timeout,
+                          notifiable)
+        lat = list(metrics.latency.samples or [])
         failed = c["notify_failed"]
+        delivered_total = c["notify_delivered"]
         svc.stop()
         await svc.shutdown()
+        d.barrier()  # every shard stopped: the sink's counts are final
 
-        ref = None
-        if args.ref_events > 0 and d.rank == 0:
-            ref = await run_reference(args, api_port, f"{scheme}://127.0.0.1:{sink_port}", cmd,
-                                      args.warmup + args.steps + 1, pki.ca_crt if pki else None)
-        replay.stdin.write(b"QUIT\n")
-        await replay.stdin.drain()
-        return {"elapsed": elapsed, "events": events, "notified": notified, "events_per_step": events_per_step,
-                "p50_ns": p50, "p99_ns": p99, "lat_samples": lat_n, "sat_p50_ns": sat_p50,
-                "failed": failed, "ref": ref,
+        verify = ref = None
+        if d.rank == 0:
+            if args.verify:
+                verify = await fx.verify_counts()
+            if args.ref_events > 0:
+                ref = await run_reference(args, fx, shared, targets, k_lat + 1)
+        return {"elapsed": elapsed, "events": events, "notified": notified,
+                "events_per_step": shared["events_per_step"], "per_step_mine": per_step, "scopes": len(mine),
+                "lat": lat, "sat": sat, "failed": failed, "ref": ref, "verify": verify,
+                "delivered_total": delivered_total, "notifiable": notifiable[0],
+                "fixture_workers": shared["fixture_workers"], "sink_workers": getattr(fx, "sink_workers", None),
                 "cpu_util": {k: round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0
                              if not k.startswith("thread_") or k == "thread_loop"},
                 "cpu_threads": sorted((round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0
                                        if k.startswith("thread_") and k != "thread_loop" and k in cpu1),
                                       reverse=True)[:8],
-                "decode_threads": decode_threads,
+                "decode_threads": decode_threads, "scope": scope,
                 "placement": {"watcher": cpu_ranges(watcher_cpus)}}
     finally:
-        for p in (replay, sink):
-            try:
-                os.killpg(p.pid, signal.SIGTERM)
-            except (ProcessLookupError, PermissionError):
-                pass
-            try:
-                await asyncio.wait_for(p.wait(), 5)
-            except asyncio.TimeoutError:
-                try:
-                    os.killpg(p.pid, signal.SIGKILL)
-                except (ProcessLookupError, PermissionError):
-                    pass
-            transport = getattr(p, "_transport", None)
-            if transport is not None:
-                transport.close()  # close pipes while the loop is alive (no __del__ noise)
+        await fx.close()
 
 
-def cpu_snapshot(replay_pid: int, sink_pid: int) -> dict:
-    """CPU seconds (user+system) of this watcher process and of the replay and
-    sink process trees — which side saturates a core tells what bounds a run."""
+async def run_latency(fx, d, svc, c, k: int, rate: float, count: int, timeout: float, notifiable: list) -> None:
+    """Pace ``count`` events of step ``k`` at ``rate`` ev/s over the whole cluster,
+    then wait until every rank has received what it was sent and drained."""
+    sent = None
+    if d.rank == 0:
+        sent = await fx.cmd(f"PACE {k} {rate} {count}")
+        notifiable[0] += int(sent[3])
+    await d.abarrier()  # the fixture has sent everything
+    deadline = time.monotonic() + timeout
+    quiet_since = time.monotonic()
+    last = c["events_received"]
+    while True:
+        if c["events_received"] != last:
+            last, quiet_since = c["events_received"], time.monotonic()
+        if svc.notifier.outstanding() == 0 and time.monotonic() - quiet_since > 0.5:
+            break
+        if time.monotonic() > deadline:
+            raise TimeoutError(f"rank {d.rank}: latency phase did not drain")
+        await asyncio.sleep(0.005)
+    await d.abarrier()
+
+
+def cpu_snapshot(fx: "Fixtures") -> dict:
+    """CPU seconds (user+system) of this watcher process and (rank 0) of the
+    replay and sink process trees — which side saturates tells what bounds a run."""
     import psutil
 
-    def tree(pid: int) -> float:
+    def tree(p) -> float:
+        if p is None:
+            return 0.0
         try:
-            root = psutil.Process(pid)
+            root = psutil.Process(p.pid)
             procs = [root] + root.children(recursive=True)
         except psutil.NoSuchProcess:
             return 0.0
@@ -337,40 +490,43 @@ def cpu_snapshot(replay_pid: int, sink_pid: int) -> dict:
         return tot
 
     t = os.times()
-    out = {"watcher": t.user + t.system, "replay": tree(replay_pid), "sink": tree(sink_pid)}
+    out = {"watcher": t.user + t.system}
+    if fx.replay is not None:
+        out["replay"] = tree(fx.replay)
+        out["sink"] = tree(fx.sink)
     main = threading.get_native_id()
     for th in psutil.Process().threads():  # per thread: the event loop vs the decode workers
         out["thread_loop" if th.id == main else f"thread_{th.id}"] = th.user_time + th.system_time
     return out
 
 
-async def run_reference(args, api_port: int, sink_url: str, cmd, step: int, ca_file=None) -> dict:
+async def run_reference(args, fx: "Fixtures", shared: dict, targets, step: int) -> dict:
     from benchmarks.reference_equiv import RefEquivWatcher
     from k8s_watcher_amd.utils.config import load_settings
 
     s = load_settings(args.profile)
-    ref = RefEquivWatcher(args.profile, s.watcher.namespaces, s.watcher.critical_events_only,
-                          sink_url, ca_file=ca_file)
+    ref = RefEquivWatcher(args.profile, targets, s.watcher.critical_events_only,
+                          shared["sink_url"], ca_file=shared["ca"])
     loop = asyncio.get_running_loop()
     connected = loop.create_future()
     result = {}
 
     def work() -> None:
-        result["elapsed"] = ref.run(f"http://127.0.0.1:{api_port}", args.ref_events,
+        result["elapsed"] = ref.run(f"http://127.0.0.1:{shared['api_port']}", args.ref_events,
                                     on_connected=lambda: loop.call_soon_threadsafe(connected.set_result, None))
 
     for _ in range(500):
-        if await cmd("WATCHERS 0") == 0:
+        if int((await fx.cmd("WATCHERS"))[2]) == 0:
             break
         await asyncio.sleep(0.01)
     th = threading.Thread(target=work, daemon=True)
     th.start()
     await connected
     for _ in range(200):
-        if await cmd("WATCHERS 0") >= 1:
+        if int((await fx.cmd("WATCHERS"))[2]) >= 1:
             break
         await asyncio.sleep(0.01)
-    await cmd(f"PACE {step} 0 {args.ref_events}")
+    await fx.cmd(f"PACE {step} 0 {args.ref_events}")
     while th.is_alive():
         await asyncio.sleep(0.01)
     lat = sorted(ref.latencies_ns)
@@ -380,6 +536,13 @@ async def run_reference(args, api_port: int, sink_url: str, cmd, step: int, ca_f
             "sat_p50_ns": p50}
 
 
+def pct(samples, q: float):
+    if not samples:
+        return None
+    s = sorted(samples)
+    return s[max(0, min(len(s) - 1, int(-(-q * len(s) // 100)) - 1))]
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     d = Dist()
@@ -387,15 +550,25 @@ def main(argv=None) -> int:
     elapsed = d.reduce(res["elapsed"], "MAX")
     events = d.reduce(float(res["events"]), "SUM")
     notified = d.reduce(float(res["notified"]), "SUM")
-    p50 = d.reduce(res["p50_ns"] or 0.0, "MAX")
-    p99 = d.reduce(res["p99_ns"] or 0.0, "MAX")
+    delivered_total = d.reduce(float(res["delivered_total"]), "SUM")
+    lat = [x for r in d.all_gather(res["lat"]) for x in r]
+    sat = [x for r in d.all_gather(res["sat"]) for x in r]
+    per_rank = d.all_gather({"events": res["events"], "scopes": res["scopes"], "elapsed": round(res["elapsed"], 4),
+                             "notified": res["notified"]})
     d.close()
     if d.rank != 0:
         return 0
     value = events / elapsed
     ref = res["ref"]
     ref_rate = ref["events_per_s"] if ref else None
-    per_rank = value / d.world
+    p50, p99, sat_p50 = pct(lat, 50), pct(lat, 99), pct(sat, 50)
+    verify = res["verify"]
+    if verify is not None:
+        verify["expected"] = res["notifiable"]
+        verify["missing"] = res["notifiable"] - verify["unique"]
+        verify["delivered_by_shards"] = int(delivered_total)
+        verify["exactly_once"] = verify["missing"] == 0 and verify["duplicates"] == 0 \
+            and verify["received"] == verify["expected"]
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -406,38 +579,46 @@ def main(argv=None) -> int:
         "ms_per_step": round(elapsed / args.steps * 1000, 3),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(per_rank / ref_rate, 2) if ref_rate else None,
+        "vs_baseline": round(value / d.world / ref_rate, 2) if ref_rate else None,
         "dtype": "n/a",
         "data": "synthetic",
         "config": {
             "model": f"k8s-watcher {args.profile} profile (BASELINE config #4: all-namespaces watch, "
-                     f"{args.pods_per_step}-pod churn, async notifier pool)",
-            "global_batch": int(res["events_per_step"] * d.world),
+                     f"{args.pods_per_step}-pod churn per rank, async notifier pool)",
+            "global_batch": int(res["events_per_step"]),
             "seq_len": None,
-            "parallelism": f"shard{d.world}" if d.world > 1 else "single-process",
+            "parallelism": (f"shard{d.world} (namespace_scope={res['scope']}, "
+                            f"{args.namespaces} namespaces, assignment={args.assignment})"
+                            if d.world > 1 else f"single-process ({res['scope']} watch)"),
             "engine": args.engine,
             "decode_threads": res["decode_threads"],
             "clusterapi": "https" if args.tls else "http",
+            "namespaces": args.namespaces,
+            "target_namespaces": len(target_namespaces(args.targets, range(args.namespaces))),
         },
         "p50_latency_ms": round(p50 / 1e6, 3) if p50 else None,
         "p99_latency_ms": round(p99 / 1e6, 3) if p99 else None,
-        "latency_rate_ev_s": args.latency_rate,
-        "latency_samples": res["lat_samples"],
+        "latency_rate_ev_s_per_rank": args.latency_rate,
+        "latency_samples": len(lat),
         "notified_per_s": round(notified / elapsed, 1),
         "notify_failed": res["failed"],
+        "verify": verify,
+        "per_rank": per_rank,
+        "fixture_workers": res["fixture_workers"],
+        "sink_workers": res["sink_workers"],
         "cpu_util_rank0": res["cpu_util"],
         "cpu_other_threads_rank0": res["cpu_threads"],
         # the watcher's own efficiency (the rate is bound by the replay fixture's core when it hits 1.0)
         "events_per_watcher_cpu_second": (round(res["events"] / (res["cpu_util"]["watcher"] * res["elapsed"]), 1)
                                           if res["cpu_util"].get("watcher") else None),
         "placement_rank0": res["placement"],
-        "saturated_p50_latency_ms": round(res["sat_p50_ns"] / 1e6, 3) if res["sat_p50_ns"] else None,
+        "saturated_p50_latency_ms": round(sat_p50 / 1e6, 3) if sat_p50 else None,
         "reference_equiv": ({"events_per_s": round(ref_rate, 1), "events": ref["events"],
                              "notified": ref["notified"],
                              "saturated_p50_latency_ms": round(ref["sat_p50_ns"] / 1e6, 3)
                              if ref["sat_p50_ns"] else None} if ref else None),
         "baseline_source": "reference-equivalent pipeline measured in this run on the same replay "
-                           "(BASELINE.md: reference publishes no numbers)",
+                           "(BASELINE.md: reference publishes no numbers; parity unpinned)",
     }
     line = json.dumps(out)
     print(line, flush=True)

@@ -1,0 +1,543 @@
+"""One logical API server over many namespaces, served by several processes.
+
+The N-rank benchmark (``bench.py --gpus N``) runs the product's sharded
+scale-out: every rank is one watcher shard (``watcher.shard``) that opens pod
+watches only for the namespaces it owns (``namespace_scope: discover``,
+``engine/namespaces.py``). They must all watch the *same* cluster, or the
+scaling curve measures nothing but independent copies. This fixture is that
+cluster:
+
+* a deterministic event history: ``--pods`` pod lifecycles per step (ADDED →
+  3×MODIFIED → DELETED, ≈4 KB of real-shaped Pod JSON per event), spread
+  round-robin over ``--namespaces`` namespaces and interleaved in one global
+  order with one global resourceVersion sequence, as etcd would;
+* served by ``--workers`` processes that each ``listen()`` on the same port
+  with ``SO_REUSEPORT`` — the kernel spreads the watch connections, so the
+  fixture is not one core feeding N watchers;
+* any namespace watch (``/api/v1/namespaces/<ns>/pods``), the cluster-wide
+  watch (``/api/v1/pods``), LISTs of both, ``/api/v1/namespaces`` (LIST and a
+  quiet WATCH) and ``/version``.
+
+Rendering is byte splicing, not JSON work. Each pod is stamped from one of
+``--prototypes`` lifecycles (namespace, name and uid spliced in once per scope
+when its first watch arrives); per step only the resourceVersion (always 9
+digits) and the first 8 hex digits of each uid (the step number — pods are
+re-created with fresh uids every step) change, so a step of a scope is its
+base bytes with fixed-width fields overwritten, vectorised with numpy into a
+memory file, ``ahead`` steps in advance on a helper thread. A step then costs
+one ``sendfile()`` per watch connection.
+
+Control (stdin lines → one stdout line each), forwarded to every worker::
+
+    READY {json: port, events_per_step, notifiable_per_step, namespaces}
+    PREPARE <k0> <k1>          render steps [k0, k1) for the open watches -> OK
+    STEP <k>                   stream step k to every watch       -> SENT k <events> <notifiable>
+    PACE <k> <rate> <count>    first <count> events of step k at <rate>/s (0 = max) -> SENT k n m
+    WATCHERS                   -> SENT - <open watch streams over all workers>
+    QUIT
+
+``notifiable`` counts the events the production profile notifies: critical
+(DELETED or a terminal phase) and in one of ``--targets``.
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import mmap
+import os
+import random
+import socket
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+from typing import Dict, List, Optional, Tuple
+from urllib.parse import parse_qs, urlsplit
+
+import numpy as np
+
+from .podgen import PodFactory
+
+RV0 = 100_000_000  # every resourceVersion has exactly 9 digits
+RV_DIGITS = 9
+STEP_HEX = 8  # uid prefix: the step number
+_TYPES = (b'{"type":"ADDED","object":', b'{"type":"MODIFIED","object":', b'{"type":"MODIFIED","object":',
+          b'{"type":"MODIFIED","object":', b'{"type":"DELETED","object":')
+_HDR = b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked\r\n\r\n"
+_NS_PH, _NAME_PH, _UID_PH = b"@@NS@@", b"@@NAME@@", b"@@UID@@"
+_RV_FIELD = b'"resourceVersion":"' + b"0" * RV_DIGITS + b'"'
+TERMINAL = ("Succeeded", "Failed")
+
+
+def namespace_names(n: int) -> List[str]:
+    return [f"tenant-{i:03d}" for i in range(n)]
+
+
+def pod_uid(step: int, pod: int) -> bytes:
+    return b"%08x-0000-4000-8000-%012x" % (step & 0xFFFFFFFF, pod)
+
+
+class ClusterModel:
+    """The cluster's per-step event history (built once, before the workers fork)."""
+
+    def __init__(self, namespaces: List[str], pods: int, seed: int = 0, prototypes: int = 256,
+                 targets: Optional[List[str]] = None, interleave: int = 64) -> None:
+        self.namespaces = list(namespaces)
+        self.pods = pods
+        f = PodFactory(seed, ["proto-ns"])
+        self.protos: List[List[bytes]] = []  # [proto][stage] -> object JSON with placeholders
+        self.proto_phase: List[List[str]] = []
+        self.name_prefix: List[str] = []
+        for _ in range(min(prototypes, max(1, pods))):
+            lc = f.lifecycle()
+            md0 = lc[0][1]["metadata"]
+            name, uid = md0["name"], md0["uid"]
+            self.name_prefix.append(name[:-5])
+            stages, phases = [], []
+            for _et, obj in lc:
+                obj["metadata"]["resourceVersion"] = "0" * RV_DIGITS
+                obj["metadata"]["namespace"] = "@@NS@@"
+                obj["metadata"]["name"] = "@@NAME@@"
+                raw = json.dumps(obj, separators=(",", ":"), ensure_ascii=False).encode("utf-8")
+                stages.append(raw.replace(uid.encode(), _UID_PH))
+                phases.append((obj.get("status") or {}).get("phase") or "")
+            self.protos.append(stages)
+            self.proto_phase.append(phases)
+        # global order: `interleave` lifecycles in flight, a seeded random pick each time
+        rng = random.Random(seed + 1)
+        order_pod, order_stage = [], []
+        active: List[List[int]] = []  # [pod, next stage]
+        made = 0
+        while made < pods or active:
+            while made < pods and len(active) < interleave:
+                active.append([made, 0])
+                made += 1
+            i = rng.randrange(len(active))
+            p = active[i]
+            order_pod.append(p[0])
+            order_stage.append(p[1])
+            p[1] += 1
+            if p[1] == 5:
+                active.pop(i)
+        self.ev_pod = np.array(order_pod, dtype=np.int64)
+        self.ev_stage = np.array(order_stage, dtype=np.int8)
+        self.E = len(order_pod)
+        n_ns = len(self.namespaces)
+        self.ev_ns = (self.ev_pod % n_ns).astype(np.int32)
+        proto = self.ev_pod % len(self.protos)
+        phase_terminal = np.array([[ph in TERMINAL for ph in stages] for stages in self.proto_phase])
+        critical = (self.ev_stage == 4) | phase_terminal[proto, self.ev_stage]
+        tset = set(targets if targets is not None else self.namespaces)
+        is_target = np.array([ns in tset for ns in self.namespaces])
+        self.notifiable = critical & is_target[self.ev_ns]
+        self.ns_index = {ns: i for i, ns in enumerate(self.namespaces)}
+
+    def events_in(self, ns: str) -> int:
+        return int(np.count_nonzero(self.ev_ns == self.ns_index[ns]))
+
+    def notifiable_upto(self, count: int) -> int:
+        return int(np.count_nonzero(self.notifiable[:count]))
+
+    def event_obj(self, g: int) -> bytes:
+        """Object JSON of global event ``g`` with step 0 / RV placeholders (list & backlog paths)."""
+        pod = int(self.ev_pod[g])
+        ns = self.namespaces[int(self.ev_ns[g])].encode()
+        p = pod % len(self.protos)
+        name = f"{self.name_prefix[p]}{pod:05x}".encode()
+        raw = self.protos[p][int(self.ev_stage[g])]
+        return raw.replace(_NS_PH, ns).replace(_NAME_PH, name).replace(_UID_PH, pod_uid(0, pod))
+
+    def compile(self, scope: str) -> "ScopeStream":
+        gidx = (np.arange(self.E, dtype=np.int64) if scope == "*"
+                else np.flatnonzero(self.ev_ns == self.ns_index[scope]).astype(np.int64))
+        parts: List[bytes] = []
+        ev_off = np.zeros(len(gidx) + 1, dtype=np.int64)
+        rv_off = np.zeros(len(gidx), dtype=np.int64)
+        uid_off: List[int] = []
+        pos = 0
+        for j, g in enumerate(gidx.tolist()):
+            body = _TYPES[int(self.ev_stage[g])] + self.event_obj(g) + b"}\n"
+            head = b"%x\r\n" % len(body)
+            chunk = head + body + b"\r\n"
+            base = pos + len(head)
+            k = body.find(_RV_FIELD)
+            rv_off[j] = base + k + len(_RV_FIELD) - 1 - RV_DIGITS
+            uid = pod_uid(0, int(self.ev_pod[g]))
+            k = body.find(uid)
+            while k >= 0:
+                uid_off.append(base + k)
+                k = body.find(uid, k + 1)
+            parts.append(chunk)
+            pos += len(chunk)
+            ev_off[j + 1] = pos
+        base_buf = np.frombuffer(b"".join(parts), dtype=np.uint8)
+        return ScopeStream(scope, base_buf, ev_off, rv_off, np.array(uid_off, dtype=np.int64), gidx, self.E)
+
+
+class ScopeStream:
+    """The events of one watch scope (a namespace or ``*``) as patchable bytes."""
+
+    def __init__(self, scope: str, base: np.ndarray, ev_off: np.ndarray, rv_off: np.ndarray,
+                 uid_off: np.ndarray, gidx: np.ndarray, E: int) -> None:
+        self.scope, self.base, self.ev_off, self.rv_off = scope, base, ev_off, rv_off
+        self.uid_off, self.gidx, self.E = uid_off, gidx, E
+
+    @staticmethod
+    def _patch(buf: np.ndarray, rv_off: np.ndarray, rvs: np.ndarray, uid_off: np.ndarray, step: int) -> None:
+        v = rvs.copy()
+        for d in range(RV_DIGITS - 1, -1, -1):
+            buf[rv_off + d] = 48 + (v % 10)
+            v //= 10
+        for c, ch in enumerate(b"%08x" % (step & 0xFFFFFFFF)):
+            buf[uid_off + c] = ch
+
+    def render_into(self, out: np.ndarray, step: int) -> None:
+        np.copyto(out, self.base)
+        self._patch(out, self.rv_off, RV0 + step * self.E + self.gidx, self.uid_off, step)
+
+    def render_file(self, step: int):
+        """The whole step as a sealed memory file (for ``sendfile``)."""
+        size = len(self.base)
+        fd = os.memfd_create(f"replay-{self.scope}-{step}")
+        os.ftruncate(fd, max(1, size))
+        with mmap.mmap(fd, max(1, size)) as mm:
+            if size:
+                self.render_into(np.frombuffer(mm, dtype=np.uint8, count=size), step)
+        return open(fd, "rb", buffering=0), size
+
+    def event_bytes(self, step: int, j: int) -> bytes:
+        a, b = int(self.ev_off[j]), int(self.ev_off[j + 1])
+        buf = self.base[a:b].copy()
+        lo, hi = np.searchsorted(self.uid_off, [a, b])
+        self._patch(buf, self.rv_off[j:j + 1] - a, RV0 + step * self.E + self.gidx[j:j + 1],
+                    self.uid_off[lo:hi] - a, step)
+        return buf.tobytes()
+
+    def locate(self, g0: int, g1: int) -> Tuple[int, int]:
+        """Local event range of global events [g0, g1)."""
+        return int(np.searchsorted(self.gidx, g0)), int(np.searchsorted(self.gidx, g1))
+
+
+class Worker:
+    """One serving process: its share of the watch connections, every command."""
+
+    def __init__(self, model: ClusterModel, sock: socket.socket, ahead: int) -> None:
+        self.m = model
+        self.sock = sock
+        self.ahead = ahead
+        self.scopes: Dict[str, ScopeStream] = {}
+        self.watchers: List[Tuple[str, asyncio.StreamWriter]] = []
+        self.sent: List[List[int]] = []  # [step, g0, g1) ranges of the global history sent so far
+        self.rv = RV0 - 1
+        self.rendered: Dict[Tuple[str, int], "asyncio.Future"] = {}
+        self.pool = ThreadPoolExecutor(2, thread_name_prefix="render")
+
+    # ------------------------------------------------------------------ state
+    def scope(self, name: str) -> ScopeStream:
+        s = self.scopes.get(name)
+        if s is None:
+            s = self.scopes[name] = self.m.compile(name)
+        return s
+
+    def _advance(self, step: int, g0: int, g1: int) -> None:
+        if self.sent and self.sent[-1][0] == step and self.sent[-1][2] == g0:
+            self.sent[-1][2] = g1
+        else:
+            self.sent.append([step, g0, g1])
+        self.rv = RV0 + step * self.m.E + g1 - 1
+
+    def _history(self, scope: ScopeStream, since: int):
+        """(step, local index) of this scope's events sent with resourceVersion > ``since``."""
+        for step, g0, g1 in self.sent:
+            lo, hi = scope.locate(g0, g1)
+            for j in range(lo, hi):
+                if RV0 + step * self.m.E + int(scope.gidx[j]) > since:
+                    yield step, j
+
+    def list_body(self, name: str) -> bytes:
+        sc = self.scope(name)
+        live: Dict[int, Tuple[int, int]] = {}
+        for step, j in self._history(sc, -1):
+            g = int(sc.gidx[j])
+            key = (step, int(self.m.ev_pod[g]))
+            if self.m.ev_stage[g] == 4:
+                live.pop(key, None)
+            else:
+                live[key] = (step, j)
+        items = []
+        for step, j in live.values():
+            ev = sc.event_bytes(step, j)
+            body = ev[ev.index(b"\r\n") + 2:-2]
+            items.append(body[body.index(b'"object":') + 9:-2])
+        return (b'{"kind":"PodList","apiVersion":"v1","metadata":{"resourceVersion":"%d"},"items":[%s]}'
+                % (self.rv, b",".join(items)))
+
+    # ------------------------------------------------------------------ HTTP
+    async def handle(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
+        try:
+            while True:
+                line = await reader.readline()
+                if not line:
+                    return
+                while True:
+                    h = await reader.readline()
+                    if h in (b"\r\n", b"\n", b""):
+                        break
+                u = urlsplit(line.split()[1].decode())
+                q = {k: v[-1] for k, v in parse_qs(u.query).items()}
+                watch = q.get("watch", "").lower() in ("true", "1")
+                path = u.path
+                if path == "/version":
+                    body = b'{"major":"1","minor":"33","gitVersion":"v1.33.1-cluster-replay"}'
+                elif path == "/api/v1/namespaces":
+                    if watch:  # the namespace set never changes here: a quiet watch
+                        writer.write(_HDR)
+                        await reader.read()
+                        return
+                    body = json.dumps({"kind": "NamespaceList", "apiVersion": "v1",
+                                       "metadata": {"resourceVersion": str(RV0 - 1)},
+                                       "items": [{"metadata": {"name": n}} for n in self.m.namespaces]}).encode()
+                elif path == "/api/v1/pods" or (path.startswith("/api/v1/namespaces/") and path.endswith("/pods")):
+                    name = "*" if path == "/api/v1/pods" else path.split("/")[4]
+                    if name != "*" and name not in self.m.ns_index:
+                        body = b'{"kind":"PodList","apiVersion":"v1","metadata":{"resourceVersion":"%d"},' \
+                               b'"items":[]}' % self.rv
+                    elif watch:
+                        self.start_watch(name, writer, q.get("resourceVersion"))
+                        await reader.read()  # hold until the client goes away
+                        return
+                    else:
+                        body = self.list_body(name)
+                else:
+                    writer.write(b"HTTP/1.1 404 Not Found\r\nContent-Length: 0\r\n\r\n")
+                    await writer.drain()
+                    continue
+                writer.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n"
+                             % len(body) + body)
+                await writer.drain()
+        except (ConnectionError, asyncio.IncompleteReadError):
+            return
+        finally:
+            self.watchers = [(s, w) for s, w in self.watchers if w is not writer]
+            writer.close()
+
+    def start_watch(self, name: str, writer: asyncio.StreamWriter, rv_param: Optional[str]) -> None:
+        """Synchronous: backlog and registration happen between two sends."""
+        writer.write(_HDR)
+        if name in self.m.ns_index or name == "*":
+            sc = self.scope(name)
+            since = int(rv_param) if rv_param not in (None, "", "0") else -1
+            if since < 0:
+                # no resourceVersion: synthetic ADDED for the live pods (as kube-apiserver)
+                body = self.list_body(name)
+                start = body.index(b'"items":[') + 9
+                # the list items are object JSON; re-frame each as an ADDED event
+                for obj in _split_items(body[start:-2]):
+                    ev = _TYPES[0] + obj + b"}\n"
+                    writer.write(b"%x\r\n%s\r\n" % (len(ev), ev))
+            else:
+                for step, j in self._history(sc, since):
+                    writer.write(sc.event_bytes(step, j))
+        self.watchers.append((name, writer))
+
+    # ------------------------------------------------------------------ streaming
+    def _targets(self) -> List[Tuple[str, asyncio.StreamWriter]]:
+        return [(s, w) for s, w in self.watchers if not w.is_closing()]
+
+    def _ensure(self, name: str, step: int) -> "asyncio.Future":
+        key = (name, step)
+        fut = self.rendered.get(key)
+        if fut is None:
+            sc = self.scope(name)
+            fut = self.rendered[key] = asyncio.get_running_loop().run_in_executor(self.pool, sc.render_file, step)
+        return fut
+
+    async def prepare(self, k0: int, k1: int) -> None:
+        names = sorted({s for s, _ in self._targets()})
+        futs = [self._ensure(n, k) for k in range(k0, k1) for n in names]
+        if futs:
+            await asyncio.gather(*futs)
+
+    async def step(self, k: int) -> None:
+        targets = self._targets()
+        self._advance(k, 0, self.m.E)  # before the first await: a watch joining now gets it as backlog
+        names = sorted({s for s, _ in targets})
+        files = {n: await self._ensure(n, k) for n in names}
+        for n in names:  # keep `ahead` steps rendered in advance
+            self._ensure(n, k + self.ahead)
+        loop = asyncio.get_running_loop()
+        try:
+            res = await asyncio.gather(*(loop.sendfile(w.transport, files[n][0], 0, files[n][1])
+                                         for n, w in targets if files[n][1]), return_exceptions=True)
+            for r in res:
+                if isinstance(r, BaseException) and not isinstance(r, (ConnectionError, RuntimeError)):
+                    raise r
+        finally:
+            for n in names:
+                files[n][0].close()
+                self.rendered.pop((n, k), None)
+
+    async def pace(self, k: int, rate: float, count: int) -> None:
+        t0 = time.monotonic()
+        ev_ns = self.m.ev_ns
+        nss = self.m.namespaces
+        for g in range(count):
+            self._advance(k, g, g + 1)
+            ns = nss[int(ev_ns[g])]
+            for s, w in self._targets():
+                if s == ns or s == "*":
+                    sc = self.scope(s)
+                    j = int(np.searchsorted(sc.gidx, g))
+                    w.write(sc.event_bytes(k, j))
+            if rate:
+                delay = t0 + (g + 1) / rate - time.monotonic()
+                if delay > 0:
+                    await asyncio.sleep(delay)
+            elif g % 256 == 255:
+                await asyncio.sleep(0)
+        for _, w in self._targets():
+            try:
+                await w.drain()
+            except ConnectionError:
+                pass
+
+    async def serve(self, ctrl_in: int, ctrl_out: int) -> None:
+        loop = asyncio.get_running_loop()
+        server = await asyncio.start_server(self.handle, sock=self.sock, limit=1 << 20)
+        reader = asyncio.StreamReader()
+        await loop.connect_read_pipe(lambda: asyncio.StreamReaderProtocol(reader), os.fdopen(ctrl_in, "rb"))
+        out = os.fdopen(ctrl_out, "wb", buffering=0)
+        out.write(b"READY\n")
+        while True:
+            line = await reader.readline()
+            if not line:
+                break
+            parts = line.decode().split()
+            cmd = parts[0].upper() if parts else ""
+            reply = "OK"
+            if cmd == "QUIT":
+                break
+            if cmd == "PREPARE":
+                await self.prepare(int(parts[1]), int(parts[2]))
+            elif cmd == "STEP":
+                await self.step(int(parts[1]))
+            elif cmd == "PACE":
+                await self.pace(int(parts[1]), float(parts[2]), min(int(parts[3]), self.m.E))
+            elif cmd == "WATCHERS":
+                reply = str(len(self._targets()))
+            out.write(reply.encode() + b"\n")
+        server.close()
+        self.pool.shutdown(wait=False, cancel_futures=True)
+
+
+def _split_items(arr: bytes) -> List[bytes]:
+    """Split the concatenated objects of a PodList ``items`` array (no nesting at top level)."""
+    out, depth, start, in_str, esc = [], 0, 0, False, False
+    for i, ch in enumerate(arr):
+        if in_str:
+            if esc:
+                esc = False
+            elif ch == 0x5C:
+                esc = True
+            elif ch == 0x22:
+                in_str = False
+        elif ch == 0x22:
+            in_str = True
+        elif ch == 0x7B:
+            if depth == 0:
+                start = i
+            depth += 1
+        elif ch == 0x7D:
+            depth -= 1
+            if depth == 0:
+                out.append(arr[start:i + 1])
+    return out
+
+
+def _reuseport_socket(port: int, listen: bool) -> socket.socket:
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+    s.bind(("127.0.0.1", port))
+    if listen:
+        s.listen(1024)
+        s.setblocking(False)
+    return s
+
+
+def run(args) -> None:
+    namespaces = (args.namespace_list.split(",") if args.namespace_list
+                  else namespace_names(args.namespaces))
+    targets = args.targets.split(",") if args.targets else None
+    model = ClusterModel(namespaces, args.pods, args.seed, args.prototypes, targets)
+    reserve = _reuseport_socket(args.port, listen=False)  # holds the port; workers listen on it
+    port = reserve.getsockname()[1]
+    workers = []  # (pid, ctrl_w, reply_r)
+    for _ in range(max(1, args.workers)):
+        c_r, c_w = os.pipe()
+        r_r, r_w = os.pipe()
+        pid = os.fork()
+        if pid == 0:
+            os.close(c_w)
+            os.close(r_r)
+            reserve.close()
+            try:
+                asyncio.run(Worker(model, _reuseport_socket(port, listen=True), args.ahead).serve(c_r, r_w))
+            finally:
+                os._exit(0)
+        os.close(c_r)
+        os.close(r_w)
+        workers.append((pid, os.fdopen(c_w, "wb", buffering=0), os.fdopen(r_r, "rb", buffering=0)))
+    for _, _, rd in workers:
+        assert rd.readline().strip() == b"READY"
+    info = {"port": port, "events_per_step": model.E, "notifiable_per_step": model.notifiable_upto(model.E),
+            "namespaces": {ns: model.events_in(ns) for ns in namespaces}, "workers": len(workers)}
+    print("READY " + json.dumps(info, separators=(",", ":")), flush=True)
+    for line in sys.stdin:
+        parts = line.split()
+        if not parts:
+            continue
+        cmd = parts[0].upper()
+        for _, wr, _ in workers:
+            wr.write(line.encode() if line.endswith("\n") else (line + "\n").encode())
+        if cmd == "QUIT":
+            break
+        replies = [rd.readline().decode().strip() for _, _, rd in workers]
+        if cmd == "STEP":
+            print(f"SENT {parts[1]} {model.E} {model.notifiable_upto(model.E)}", flush=True)
+        elif cmd == "PACE":
+            n = min(int(parts[3]), model.E)
+            print(f"SENT {parts[1]} {n} {model.notifiable_upto(n)}", flush=True)
+        elif cmd == "WATCHERS":
+            print(f"SENT - {sum(int(r) for r in replies)}", flush=True)
+        else:
+            print("OK", flush=True)
+    for pid, wr, _ in workers:
+        try:
+            wr.write(b"QUIT\n")
+        except BrokenPipeError:
+            pass
+    for pid, _, _ in workers:
+        try:
+            os.waitpid(pid, 0)
+        except ChildProcessError:
+            pass
+
+
+def main(argv: Optional[List[str]] = None) -> None:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--port", type=int, default=0)
+    ap.add_argument("--pods", type=int, default=10000, help="pod lifecycles per step, whole cluster")
+    ap.add_argument("--namespaces", type=int, default=64)
+    ap.add_argument("--namespace-list", default=None, help="comma-separated names instead of tenant-NNN")
+    ap.add_argument("--targets", default=None, help="namespaces the watchers notify for (notifiable counts)")
+    ap.add_argument("--workers", type=int, default=2)
+    ap.add_argument("--prototypes", type=int, default=256)
+    ap.add_argument("--ahead", type=int, default=2, help="steps rendered in advance per watched scope")
+    ap.add_argument("--seed", type=int, default=0)
+    run(ap.parse_args(argv))
+
+
+if __name__ == "__main__":
+    main()

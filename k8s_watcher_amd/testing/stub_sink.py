@@ -238,7 +238,8 @@ def run_sink_process(port: int, workers: int = 1, latency: float = 0.0,
     """Blocking: serve on ``port`` with ``workers`` SO_REUSEPORT processes (bench helper).
 
     With ``verify_dir`` every worker records ``uid|event_type|phase`` counts and
-    writes them to ``verify_dir/sink-<pid>.json`` on SIGTERM.
+    writes them to ``verify_dir/sink-<pid>.json`` on SIGTERM (and, without
+    stopping, on SIGUSR1).
     """
     import signal as _signal
     pids = []
@@ -261,14 +262,20 @@ def run_sink_process(port: int, workers: int = 1, latency: float = 0.0,
         await sink.start("127.0.0.1", port, reuse_port=True, ssl_context=ctx)
         stop = asyncio.Event()
         loop = asyncio.get_running_loop()
-        loop.add_signal_handler(_signal.SIGTERM, stop.set)
-        await stop.wait()
-        if verify_dir:
+
+        def dump() -> None:
             st = sink.state
             final = os.path.join(verify_dir, f"sink-{os.getpid()}.json")
             with open(final + ".tmp", "w") as fh:  # renamed when complete: readers never see a partial dump
                 json.dump({"count": st.count, "keys": {k.decode(): v for k, v in st.keys.items()}}, fh)
             os.replace(final + ".tmp", final)
+
+        loop.add_signal_handler(_signal.SIGTERM, stop.set)
+        if verify_dir:
+            loop.add_signal_handler(_signal.SIGUSR1, dump)  # a snapshot while still serving
+        await stop.wait()
+        if verify_dir:
+            dump()
 
     try:
         asyncio.run(serve())

@@ -107,20 +107,47 @@ def test_launcher_two_shards_exactly_once(tmp_path):
     assert "Shard 0/2" in err and "Shard 1/2" in err
 
 
-def test_bench_two_ranks_gloo():
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_bench_sharded_ranks_exactly_once(ranks):
+    """bench.py --gpus N is the product's sharded scale-out: N shard processes
+    (gloo ranks) against ONE cluster fixture; each watches only the namespaces
+    it owns, the shared verify-mode sink proves the union is exactly-once."""
     port = free_port()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--pods-per-step", "300",
-                        "--ref-events", "0", "--latency-seconds", "0.5", "--sink-workers", "1"],
+                        "--gpus", str(ranks), "--steps", "2", "--warmup", "1", "--pods-per-step", "300",
+                        "--namespaces", "16", "--ref-events", "0", "--latency-seconds", "0.5",
+                        "--sink-workers", "2", "--fixture-workers", "2", "--no-placement",
+                        "--decode-threads", "0"],
                        capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1  # rank 0 only
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * 1500
+    assert d["n_gpus"] == ranks and d["config"]["global_batch"] == ranks * 1500
     assert d["value"] > 0 and d["scaling"] == "weak"
+    assert "namespace_scope=discover" in d["config"]["parallelism"]
+    # every shard watched its own namespaces: 16 in total, split evenly, each event counted once
+    assert sum(p["scopes"] for p in d["per_rank"]) == 16
+    assert {p["scopes"] for p in d["per_rank"]} == {16 // ranks}
+    assert sum(p["events"] for p in d["per_rank"]) == 2 * ranks * 1500
+    v = d["verify"]
+    assert v["exactly_once"] and v["duplicates"] == 0 and v["missing"] == 0, v
+    assert v["expected"] == v["delivered_by_shards"] > 0
+
+
+def test_bench_single_rank_cluster_watch():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--pods-per-step", "300", "--namespaces", "8", "--ref-events", "200",
+                        "--latency-seconds", "0.5", "--sink-workers", "1", "--no-placement"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["n_gpus"] == 1 and d["config"]["parallelism"] == "single-process (cluster watch)"
+    assert d["per_rank"][0]["events"] == 2 * 1500
+    assert d["verify"]["exactly_once"]
+    assert d["reference_equiv"]["events"] == 200 and d["vs_baseline"] > 0
 
 
 def test_balanced_assignment_bounded_and_stable():
