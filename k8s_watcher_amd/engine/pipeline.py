@@ -88,6 +88,8 @@ class EventPipeline:
             w.event_timestamp == "utc", core, False, False, decode)
         if w.payload_extra:
             self.native.set_extra(w.payload_extra)
+        if self.elog.native_sink is not None:
+            self.native.set_log_sink(self.elog.native_sink)  # per-event lines formatted in C++
 
     def handle_raw(self, data: bytes, read_ns: int, framed: bool) -> List[tuple]:
         """Native path: raw watch bytes (HTTP-chunk framed or not) → everything

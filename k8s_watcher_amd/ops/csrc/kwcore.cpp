@@ -24,6 +24,7 @@
 #include <openssl/x509v3.h>
 
 #include <linux/futex.h>
+#include <poll.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
@@ -1863,6 +1864,7 @@ PyObject* kw_bench_parse(PyObject*, PyObject* args) {
 }
 
 #include "podcache.inc"
+#include "logsink.inc"
 #include "engine.inc"
 
 PyMethodDef module_methods[] = {
@@ -1900,7 +1902,8 @@ PyMODINIT_FUNC PyInit__kwcore(void) {
     if (PyType_Ready(&ScannerType) < 0) return nullptr;
     Py_INCREF(&ScannerType);
     PyModule_AddObject(m, "ResponseScanner", (PyObject*)&ScannerType);
-    if (register_engine(m) < 0 || register_podcache(m) < 0 || register_pipeline(m) < 0) return nullptr;
+    if (register_engine(m) < 0 || register_podcache(m) < 0 || register_pipeline(m) < 0 || register_logsink(m) < 0)
+        return nullptr;
     const char* names[6] = {"ADDED", "MODIFIED", "DELETED", "BOOKMARK", "ERROR", "INVALID"};
     for (int i = 0; i < 6; ++i) {
         g_types[i] = PyUnicode_InternFromString(names[i]);

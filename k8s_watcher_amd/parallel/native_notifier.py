@@ -75,6 +75,8 @@ class NativeNotifierPool:
             head.encode("latin-1"), settings.pool.connections, settings.pool.pipeline_depth, r.max_attempts,
             r.delay_seconds, r.multiplier, r.max_delay_seconds, settings.pool.coalesce, log_events,
             sorted(RETRYABLE_STATUS), self.metrics.c)
+        if self.elog.native_sink is not None:
+            self.core.set_log_sink(self.elog.native_sink)  # delivery lines formatted in C++
         # histograms accumulate in C++; raw samples only when the Metrics keep them (benchmarks)
         self.core.set_histograms(_BUCKETS_NS, self.metrics.record_samples)
         self.metrics.latency.add_source(lambda: self._hist(0))
@@ -318,6 +320,8 @@ class NativeNotifierPool:
                 else:
                     self.log.error(msg)
             elog.flush()
+        elif self.elog.native_sink is not None:
+            self.elog.flush()  # delivery lines the core wrote into the native sink
         if lat:
             self.metrics.latency.add_samples(array.array("q", lat))
         for i in need_connect:

@@ -22,15 +22,16 @@ Rendering is byte splicing, not JSON work. Each pod is stamped from one of
 ``--prototypes`` lifecycles (namespace, name and uid spliced in once per scope
 when its first watch arrives); per step only the resourceVersion (always 9
 digits) and the first 8 hex digits of each uid (the step number — pods are
-re-created with fresh uids every step) change, so a step of a scope is its
-base bytes with fixed-width fields overwritten, vectorised with numpy into a
-memory file, ``ahead`` steps in advance on a helper thread. A step then costs
-one ``sendfile()`` per watch connection.
+re-created with fresh uids every step) change. So every scope keeps ONE
+buffer of its events and a step overwrites those fixed-width fields in place
+(vectorised with numpy, a few bytes per event) before the buffer is written
+to each of the scope's watch connections: per event the fixture does one
+copy into the kernel, as a real API server's watch cache would.
 
 Control (stdin lines → one stdout line each), forwarded to every worker::
 
     READY {json: port, events_per_step, notifiable_per_step, namespaces}
-    PREPARE <k0> <k1>          render steps [k0, k1) for the open watches -> OK
+    PREPARE <k0> <k1>          compile the open watches' scopes ahead of the first step -> OK
     STEP <k>                   stream step k to every watch       -> SENT k <events> <notifiable>
     PACE <k> <rate> <count>    first <count> events of step k at <rate>/s (0 = max) -> SENT k n m
     WATCHERS                   -> SENT - <open watch streams over all workers>
@@ -45,13 +46,11 @@ from __future__ import annotations
 import argparse
 import asyncio
 import json
-import mmap
 import os
 import random
 import socket
 import sys
 import time
-from concurrent.futures import ThreadPoolExecutor
 from typing import Dict, List, Optional, Tuple
 from urllib.parse import parse_qs, urlsplit
 
@@ -182,6 +181,8 @@ class ScopeStream:
                  uid_off: np.ndarray, gidx: np.ndarray, E: int) -> None:
         self.scope, self.base, self.ev_off, self.rv_off = scope, base, ev_off, rv_off
         self.uid_off, self.gidx, self.E = uid_off, gidx, E
+        self.buf: Optional[np.ndarray] = None  # patched in place per step (render)
+        self.buf_step = -1
 
     @staticmethod
     def _patch(buf: np.ndarray, rv_off: np.ndarray, rvs: np.ndarray, uid_off: np.ndarray, step: int) -> None:
@@ -192,19 +193,14 @@ class ScopeStream:
         for c, ch in enumerate(b"%08x" % (step & 0xFFFFFFFF)):
             buf[uid_off + c] = ch
 
-    def render_into(self, out: np.ndarray, step: int) -> None:
-        np.copyto(out, self.base)
-        self._patch(out, self.rv_off, RV0 + step * self.E + self.gidx, self.uid_off, step)
-
-    def render_file(self, step: int):
-        """The whole step as a sealed memory file (for ``sendfile``)."""
-        size = len(self.base)
-        fd = os.memfd_create(f"replay-{self.scope}-{step}")
-        os.ftruncate(fd, max(1, size))
-        with mmap.mmap(fd, max(1, size)) as mm:
-            if size:
-                self.render_into(np.frombuffer(mm, dtype=np.uint8, count=size), step)
-        return open(fd, "rb", buffering=0), size
+    def render(self, step: int) -> memoryview:
+        """The whole step: the scope's one buffer, its fixed-width fields set for ``step``."""
+        if self.buf is None:
+            self.buf = self.base.copy()
+        if self.buf_step != step:
+            self._patch(self.buf, self.rv_off, RV0 + step * self.E + self.gidx, self.uid_off, step)
+            self.buf_step = step
+        return memoryview(self.buf)
 
     def event_bytes(self, step: int, j: int) -> bytes:
         a, b = int(self.ev_off[j]), int(self.ev_off[j + 1])
@@ -222,16 +218,14 @@ class ScopeStream:
 class Worker:
     """One serving process: its share of the watch connections, every command."""
 
-    def __init__(self, model: ClusterModel, sock: socket.socket, ahead: int) -> None:
+    def __init__(self, model: ClusterModel, sock: socket.socket, slice_bytes: int = 1 << 20) -> None:
         self.m = model
         self.sock = sock
-        self.ahead = ahead
+        self.slice = slice_bytes
         self.scopes: Dict[str, ScopeStream] = {}
         self.watchers: List[Tuple[str, asyncio.StreamWriter]] = []
         self.sent: List[List[int]] = []  # [step, g0, g1) ranges of the global history sent so far
         self.rv = RV0 - 1
-        self.rendered: Dict[Tuple[str, int], "asyncio.Future"] = {}
-        self.pool = ThreadPoolExecutor(2, thread_name_prefix="render")
 
     # ------------------------------------------------------------------ state
     def scope(self, name: str) -> ScopeStream:
@@ -345,38 +339,26 @@ class Worker:
     def _targets(self) -> List[Tuple[str, asyncio.StreamWriter]]:
         return [(s, w) for s, w in self.watchers if not w.is_closing()]
 
-    def _ensure(self, name: str, step: int) -> "asyncio.Future":
-        key = (name, step)
-        fut = self.rendered.get(key)
-        if fut is None:
-            sc = self.scope(name)
-            fut = self.rendered[key] = asyncio.get_running_loop().run_in_executor(self.pool, sc.render_file, step)
-        return fut
-
     async def prepare(self, k0: int, k1: int) -> None:
-        names = sorted({s for s, _ in self._targets()})
-        futs = [self._ensure(n, k) for k in range(k0, k1) for n in names]
-        if futs:
-            await asyncio.gather(*futs)
+        for n in sorted({s for s, _ in self._targets()}):
+            self.scope(n).render(k0)
+
+    async def _send(self, w: asyncio.StreamWriter, view: memoryview) -> None:
+        """Write ``view`` in slices, waiting for the socket between them: the
+        transport copies at most one slice, and the scope's buffer is free to
+        be patched again once every connection's send has returned."""
+        try:
+            for i in range(0, len(view), self.slice):
+                w.write(view[i:i + self.slice])
+                await w.drain()
+        except (ConnectionError, RuntimeError):
+            pass
 
     async def step(self, k: int) -> None:
         targets = self._targets()
         self._advance(k, 0, self.m.E)  # before the first await: a watch joining now gets it as backlog
-        names = sorted({s for s, _ in targets})
-        files = {n: await self._ensure(n, k) for n in names}
-        for n in names:  # keep `ahead` steps rendered in advance
-            self._ensure(n, k + self.ahead)
-        loop = asyncio.get_running_loop()
-        try:
-            res = await asyncio.gather(*(loop.sendfile(w.transport, files[n][0], 0, files[n][1])
-                                         for n, w in targets if files[n][1]), return_exceptions=True)
-            for r in res:
-                if isinstance(r, BaseException) and not isinstance(r, (ConnectionError, RuntimeError)):
-                    raise r
-        finally:
-            for n in names:
-                files[n][0].close()
-                self.rendered.pop((n, k), None)
+        views = {n: self.scope(n).render(k) for n in {s for s, _ in targets}}
+        await asyncio.gather(*(self._send(w, views[n]) for n, w in targets))
 
     async def pace(self, k: int, rate: float, count: int) -> None:
         t0 = time.monotonic()
@@ -428,7 +410,6 @@ class Worker:
                 reply = str(len(self._targets()))
             out.write(reply.encode() + b"\n")
         server.close()
-        self.pool.shutdown(wait=False, cancel_futures=True)
 
 
 def _split_items(arr: bytes) -> List[bytes]:
@@ -483,7 +464,7 @@ def run(args) -> None:
             os.close(r_r)
             reserve.close()
             try:
-                asyncio.run(Worker(model, _reuseport_socket(port, listen=True), args.ahead).serve(c_r, r_w))
+                asyncio.run(Worker(model, _reuseport_socket(port, listen=True)).serve(c_r, r_w))
             finally:
                 os._exit(0)
         os.close(c_r)
@@ -534,7 +515,6 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--targets", default=None, help="namespaces the watchers notify for (notifiable counts)")
     ap.add_argument("--workers", type=int, default=2)
     ap.add_argument("--prototypes", type=int, default=256)
-    ap.add_argument("--ahead", type=int, default=2, help="steps rendered in advance per watched scope")
     ap.add_argument("--seed", type=int, default=0)
     run(ap.parse_args(argv))
 

@@ -16,6 +16,12 @@ rest of the event's processing.
   logger, no filters, the logger propagating to root), otherwise every call
   goes through ``logger.log`` unchanged;
 * the timestamp prefix is formatted once per millisecond.
+
+When that handler writes to a real file descriptor in UTF-8 and the native
+extension is built, :attr:`EventLog.native_sink` is a ``_kwcore.LogSink``
+(``ops/csrc/logsink.inc``) for the same fd and format: the native pipeline
+and notifier core then format their per-event lines in C++ and never hand
+them to Python at all; :meth:`EventLog.flush` writes that batch too.
 """
 
 from __future__ import annotations
@@ -29,17 +35,20 @@ from .logsetup import _HANDLER_TAG, JsonLineFormatter
 
 
 class EventLog:
-    def __init__(self, logger: logging.Logger) -> None:
+    def __init__(self, logger: logging.Logger, native: bool = True) -> None:
         self.logger = logger
         self._lines: List[str] = []
         self._handler: Optional[logging.Handler] = None
         self._prefix_ms = -1
         self._prefix = {}
+        self._native = native
+        self.native_sink = None
         self.refresh()
 
     def refresh(self) -> None:
         """Re-check whether the fast path applies (call after logging is reconfigured)."""
         self._handler = None
+        self.native_sink = None
         lg = self.logger
         root = logging.getLogger()
         if lg.handlers or lg.filters or not lg.propagate or root.filters or len(root.handlers) != 1:
@@ -63,7 +72,26 @@ class EventLog:
             return
         self._handler = h
         self._prefix_ms = -1
+        if self._native:
+            self.native_sink = self._make_native_sink(h)
 
+    def _make_native_sink(self, h: logging.StreamHandler):
+        stream = h.stream
+        try:
+            fd = stream.fileno()
+        except (AttributeError, OSError, ValueError):
+            return None  # StringIO and friends: the Python path
+        enc = (getattr(stream, "encoding", None) or "").lower().replace("-", "").replace("_", "")
+        if enc != "utf8" or getattr(h, "terminator", "\n") != "\n":
+            return None
+        try:
+            from ..ops.native import NativeUnavailable, load
+            mod = load()
+        except NativeUnavailable:
+            return None
+        json_env = self._json_env
+        return mod.LogSink(fd, json_env is not None, "" if json_env is not None else self._text_head,
+                           self.logger.name, json_env if json_env is not None else "")
     def enabled(self, level: int) -> bool:
         return self.logger.isEnabledFor(level)
 
@@ -98,8 +126,20 @@ class EventLog:
 
     def flush(self) -> None:
         lines = self._lines
+        sink = self.native_sink
+        if sink is not None and sink.pending():
+            if lines:
+                self._write(lines)
+            h = self._handler
+            if h is not None:
+                h.flush()  # nothing of Python's may sit in a buffer ahead of the native lines
+            sink.flush()
+            return
         if not lines:
             return
+        self._write(lines)
+
+    def _write(self, lines: List[str]) -> None:
         self._lines = []
         h = self._handler
         if h is None:
