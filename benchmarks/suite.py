@@ -6,8 +6,8 @@
 | # | BASELINE.json config | how it is run here |
 |---|---|---|
 | 1 | mocked API, 10 pod ADDED events, stub sink | development profile; 10 pods served by the initial LIST |
-| 2 | development.yaml, 100-pod create/delete churn | `createdelete` template: 100 pods × ADDED/MODIFIED/DELETED per step, DEBUG logging |
-| 3 | staging.yaml, single namespace, 1k pods steady, 10 ev/s MODIFIED | `steady` template: 1000 listed pods; throughput = unthrottled MODIFIED rounds, latency at 10 ev/s |
+| 2 | development.yaml, 100-pod create/delete churn | `createdelete` template: 100 pods × ADDED/MODIFIED/DELETED per round, rounds streamed back to back (sustained rate), DEBUG logging |
+| 3 | staging.yaml, single namespace, 1k pods steady, 10 ev/s MODIFIED | `steady` template: 1000 listed pods; throughput = unthrottled MODIFIED rounds streamed back to back, latency at 10 ev/s |
 | 4 | production.yaml, all namespaces, 10k-pod churn, 100 ev/s | `churn` template, 10k lifecycles per step; latency at 100 ev/s (same as bench.py) |
 | 5 | soak: RV bookmark/resume across API-server restarts, 1M events | 20 × 50k churn events with connection drops mid-step (resume), bookmarks and 410 compactions; the sink checks exactly-once |
 
@@ -119,11 +119,14 @@ class Servers:
                 await asyncio.sleep(0.1)
 
 
+EXTRA_OVERRIDES: dict = {}  # --set key.path=value, applied to every config
+
+
 async def run_ours(srv: Servers, profile: str, overrides: dict, steps: List[str], warm_steps: List[str],
                    pace: Optional[str], expect_watchers: int = 1, step_timeout: float = 300) -> dict:
-    settings = load_settings(profile, overrides=deep_merge(
+    settings = load_settings(profile, overrides=deep_merge(deep_merge(
         {"clusterapi": {"base_url": f"http://127.0.0.1:{srv.sink_port}"},
-         "watcher": {"retry": {"max_attempts": 0, "delay_seconds": 0.02}}}, overrides))
+         "watcher": {"retry": {"max_attempts": 0, "delay_seconds": 0.02}}}, overrides), EXTRA_OVERRIDES))
     m = Metrics(record_samples=True)
     t_start = time.perf_counter()
     svc = WatcherService(settings, endpoint=KubeEndpoint(server=f"http://127.0.0.1:{srv.api_port}"), metrics=m)
@@ -189,6 +192,8 @@ _STEP_RV: Dict[str, int] = {}
 
 def _last_rv(srv: Servers, s: str) -> int:
     parts = s.split()
+    if parts[0] == "STEPS":
+        return 10_000_000 + int(parts[2]) * srv.events_per_step - 1
     step = int(parts[1])
     n = srv.events_per_step if parts[0] == "STEP" else int(parts[3])
     return 10_000_000 + step * srv.events_per_step + n - 1
@@ -267,7 +272,8 @@ async def config2(a) -> dict:
     steps = max(2, int(100 * a.scale))  # 300 events per step: many steps for a stable rate
     async with Servers("createdelete", 100, prerender=steps + 1) as srv:
         e = srv.events_per_step
-        ours = await run_ours(srv, "development", {}, [f"STEP {k}" for k in range(1, steps + 1)],
+        # one stream of `steps` rounds: the sustained rate, not a stop-and-wait per 300-event round
+        ours = await run_ours(srv, "development", {}, [f"STEPS 1 {steps + 1}"],
                               ["STEP 0"], f"PACE {steps + 1} 100 {min(e, 200)}")
         ref = await run_reference(srv, "development", ["default", "kube-system"], False, e, 0,
                                   f"STEP {steps + 2}", f"PACE {steps + 3} 100 {min(e, 200)}")
@@ -278,7 +284,7 @@ async def config3(a) -> dict:
     steps = max(2, int(50 * a.scale))
     ov = {"watcher": {"namespaces": ["default"], "namespace_scope": "server"}}
     async with Servers("steady", 1000, prerender=steps + 1, namespaces="default") as srv:
-        ours = await run_ours(srv, "staging", ov, [f"STEP {k}" for k in range(1, steps + 1)], ["STEP 0"],
+        ours = await run_ours(srv, "staging", ov, [f"STEPS 1 {steps + 1}"], ["STEP 0"],
                               f"PACE {steps + 1} 10 {max(10, int(30 * a.scale))}")
         ref = await run_reference(srv, "staging", ["default"], False, 1000, 1000, f"STEP {steps + 2}",
                                   f"PACE {steps + 3} 10 {max(10, int(30 * a.scale))}")
@@ -369,7 +375,12 @@ def main(argv=None) -> int:
     ap.add_argument("--only", default="1,2,3,4,5")
     ap.add_argument("--scale", type=float, default=1.0, help="shrink step counts / sizes (tests use 0.1)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="config override for every run, e.g. clusterapi.pool.pipeline_depth=8")
     a = ap.parse_args(argv)
+    from k8s_watcher_amd.utils.config import parse_override
+    for expr in a.set:
+        EXTRA_OVERRIDES.update(deep_merge(EXTRA_OVERRIDES, parse_override(expr)))
     log_path = os.path.join(tempfile.gettempdir(), f"kw-suite-{os.getpid()}.log")
     results = {}
     for k in [int(x) for x in a.only.split(",") if x]:

@@ -54,6 +54,33 @@ class SetupError(Exception):
     """The Kubernetes client could not be set up (reference ``:246``)."""
 
 
+def required_permissions(s: Settings) -> List[tuple]:
+    """``(verb, resource, api group, namespace or None, name or None)`` this
+    configuration needs — what ``--check`` asks the API server about and what
+    ``deploy/k8s/rbac.yaml`` must grant (``tests/test_deploy.py`` holds them equal).
+
+    The reference needs list/watch on pods cluster-wide and list on namespaces
+    (``pod_watcher.py:146,264``); server-side scopes need them per namespace,
+    namespace discovery also watches namespaces, leader election its Lease."""
+    w = s.watcher
+    wanted = []
+    scopes = w.namespaces if w.namespace_scope == "server" and w.namespaces else [None]
+    for ns in scopes:
+        wanted += [("list", "pods", "", ns, None), ("watch", "pods", "", ns, None)]
+    wanted.append(("list", "namespaces", "", None, None))
+    if w.namespace_scope == "discover":
+        wanted.append(("watch", "namespaces", "", None, None))
+    le = w.leader_election
+    if le.enabled:
+        from .leader import default_lease_namespace, shard_lease
+        lease = shard_lease(s)
+        ns = lease.lease_namespace or default_lease_namespace()
+        wanted += [("get", "leases", "coordination.k8s.io", ns, lease.lease_name),
+                   ("update", "leases", "coordination.k8s.io", ns, lease.lease_name),
+                   ("create", "leases", "coordination.k8s.io", ns, None)]
+    return wanted
+
+
 class WatcherService:
     def __init__(self, settings: Settings, endpoint: Optional[KubeEndpoint] = None,
                  metrics: Optional[Metrics] = None, notifier_factory=None, serve_metrics: bool = True) -> None:
@@ -135,19 +162,7 @@ class WatcherService:
         and the clusterapi health endpoint. Logs one line per item; True if all pass."""
         assert self.api is not None
         s = self.settings
-        wanted = []
-        scopes = s.watcher.namespaces if s.watcher.namespace_scope == "server" and s.watcher.namespaces else [None]
-        for ns in scopes:
-            wanted += [("list", "pods", "", ns, None), ("watch", "pods", "", ns, None)]
-        wanted.append(("list", "namespaces", "", None, None))
-        le = s.watcher.leader_election
-        if le.enabled:
-            from .leader import default_lease_namespace, shard_lease
-            lease = shard_lease(s)
-            ns = lease.lease_namespace or default_lease_namespace()
-            wanted += [("get", "leases", "coordination.k8s.io", ns, lease.lease_name),
-                       ("update", "leases", "coordination.k8s.io", ns, lease.lease_name),
-                       ("create", "leases", "coordination.k8s.io", ns, None)]
+        wanted = required_permissions(s)
         ok = True
         for verb, res, group, ns, name in wanted:
             what = f"{verb} {group + '/' if group else ''}{res}" + (f" in {ns}" if ns else " (cluster-wide)")

@@ -25,6 +25,7 @@ Control is line-based on stdin, replies on stdout::
     READY <port> <events_per_step>
     STEP <k> [drop=<n>] [expire=<n>]  -> SENT <k> <n>  whole step; optionally abort every
                                           watch (drop) or compact + 410 them (expire) after n events
+    STEPS <a> <b>                     -> SENT <b-1> <n>  steps a..b-1 back to back (sustained stream)
     PACE <k> <rate> <count>           -> SENT <k> <n>  first <count> events at <rate>/s (rate 0 = max)
     DROP | EXPIRE | BOOKMARK          -> SENT - <watchers>
     WATCHERS                          -> SENT - <open watch streams>
@@ -407,6 +408,11 @@ async def amain(args) -> None:
         if cmd == "STEP":
             n = await srv.send(int(parts[1]), drop_at=int(opts["drop"]) if "drop" in opts else None,
                                expire_at=int(opts["expire"]) if "expire" in opts else None)
+        elif cmd == "STEPS":
+            n = 0
+            for k in range(int(parts[1]), int(parts[2])):
+                n += await srv.send(k)
+            parts[1] = str(int(parts[2]) - 1)
         elif cmd == "PACE":
             rate = float(parts[2])
             n = await srv.send(int(parts[1]), rate or None, int(parts[3]))
@@ -420,7 +426,7 @@ async def amain(args) -> None:
             n = srv.bookmark()
         else:
             n = -1
-        print(f"SENT {parts[1] if len(parts) > 1 and cmd in ('STEP', 'PACE') else '-'} {n}", flush=True)
+        print(f"SENT {parts[1] if len(parts) > 1 and cmd in ('STEP', 'STEPS', 'PACE') else '-'} {n}", flush=True)
     server.close()
 
 

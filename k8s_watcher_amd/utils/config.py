@@ -208,7 +208,7 @@ class KubernetesSettings:
 @dataclass
 class NotifierPoolSettings:
     connections: int = 16
-    pipeline_depth: int = 1
+    pipeline_depth: int = 8
     queue_size: int = 65536
     coalesce: bool = False
     native: bool = True  # C++ notifier core (watcher.engine: native)
@@ -485,7 +485,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         retry=_retry(c.get("retry"), "clusterapi.retry", RetryPolicy(3, 2.0)),
         pool=NotifierPoolSettings(
             connections=max(1, _as_int(pool.get("connections", 16), "clusterapi.pool.connections")),
-            pipeline_depth=max(1, _as_int(pool.get("pipeline_depth", 1), "clusterapi.pool.pipeline_depth")),
+            pipeline_depth=max(1, _as_int(pool.get("pipeline_depth", 8), "clusterapi.pool.pipeline_depth")),
             queue_size=max(1, _as_int(pool.get("queue_size", 65536), "clusterapi.pool.queue_size")),
             coalesce=_as_bool(pool.get("coalesce", False), "clusterapi.pool.coalesce"),
             native=_as_bool(pool.get("native", True), "clusterapi.pool.native"),

@@ -46,14 +46,62 @@ def test_empty_status_object_has_null_phase():
     assert p["status"] == {"phase": None, "conditions": [], "container_statuses": []}
 
 
-def test_python_repr_state_matches_library_pprint():
-    state = {"running": {"startedAt": "2025-07-09T01:51:32Z"}}
-    text = container_state_repr(state)
-    assert text.startswith("{'running': {'started_at': datetime.datetime(2025, 7, 9, 1, 51, 32, tzinfo=tz")
-    assert text.endswith("},\n 'terminated': None,\n 'waiting': None}")
+# Hand-derived from kubernetes==33.1.0: str(V1ContainerState) is
+# pprint.pformat(to_dict()) (model_utils to_str); to_dict keeps datetimes that
+# ApiClient.deserialize built with dateutil.parser.parse, whose repr carries
+# tzinfo=tzutc(); pprint sorts keys and wraps at width 80, one key per line,
+# nested dicts aligned after their key (/root/reference/watcher/pod_watcher.py:181).
+REPR_RUNNING = ("{'running': {'started_at': datetime.datetime(2025, 7, 9, 1, 51, 32, tzinfo=tzutc())},\n"
+                " 'terminated': None,\n"
+                " 'waiting': None}")
+REPR_WAITING = ("{'running': None,\n"
+                " 'terminated': None,\n"
+                " 'waiting': {'message': 'Back-off pulling image \"registry.example.com/app:v1\"',\n"
+                "             'reason': 'ImagePullBackOff'}}")
+# within pprint's width of 80 the dict stays on one line; 81 characters wrap
+REPR_EMPTY = "{'running': None, 'terminated': None, 'waiting': None}"
+REPR_WAITING_81 = ("{'running': None,\n"
+                   " 'terminated': None,\n"
+                   " 'waiting': {'message': None, 'reason': ''}}")
+REPR_TERMINATED = ("{'running': None,\n"
+                   " 'terminated': {'container_id': 'containerd://4f2a',\n"
+                   "                'exit_code': 137,\n"
+                   "                'finished_at': datetime.datetime(2025, 7, 9, 1, 52, 28, tzinfo=tzutc()),\n"
+                   "                'message': 'OOMKilled: memory limit 4Gi',\n"
+                   "                'reason': 'OOMKilled',\n"
+                   "                'signal': 9,\n"
+                   "                'started_at': datetime.datetime(2025, 7, 9, 1, 51, 32, tzinfo=tzutc())},\n"
+                   " 'waiting': None}")
+
+
+@pytest.mark.parametrize("state,text", [
+    ({"running": {"startedAt": "2025-07-09T01:51:32Z"}}, REPR_RUNNING),
+    ({"waiting": {"reason": "ImagePullBackOff",
+                  "message": 'Back-off pulling image "registry.example.com/app:v1"'}}, REPR_WAITING),
+    ({}, REPR_EMPTY),
+    ({"waiting": {"reason": ""}}, REPR_WAITING_81),
+    ({"terminated": {"exitCode": 137, "signal": 9, "reason": "OOMKilled", "message": "OOMKilled: memory limit 4Gi",
+                     "startedAt": "2025-07-09T01:51:32Z", "finishedAt": "2025-07-09T01:52:28Z",
+                     "containerID": "containerd://4f2a"}}, REPR_TERMINATED),
+])
+@pytest.mark.parametrize("tz", ["America/New_York", "UTC"])
+def test_python_repr_state_matches_library_to_str(state, text, tz, monkeypatch):
+    """dateutil (what the library deserialises datetimes with) returns
+    ``tzlocal()`` for a ``Z`` timestamp when the process runs in UTC, else
+    ``tzutc()``: the reference's text depends on the pod's TZ, and so does ours."""
+    import time
+    monkeypatch.setenv("TZ", tz)
+    time.tzset()
+    try:
+        if tz == "UTC":
+            text = text.replace("tzinfo=tzutc()", "tzinfo=tzlocal()")
+        assert container_state_repr(state) == text
+    finally:
+        monkeypatch.undo()
+        time.tzset()
     p = build_payload_dict({"metadata": {}, "status": {"containerStatuses": [{"name": "c", "state": state}]}},
                            "production", state_format="python_repr")
-    assert p["status"]["container_statuses"][0]["state"] == text
+    assert p["status"]["container_statuses"][0]["state"] == container_state_repr(state)
 
 
 @pytest.mark.parametrize("raw,iso", [

@@ -113,13 +113,13 @@ def test_bench_sharded_ranks_exactly_once(ranks):
     (gloo ranks) against ONE cluster fixture; each watches only the namespaces
     it owns, the shared verify-mode sink proves the union is exactly-once."""
     port = free_port()
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", BENCH_DEBUG="1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
                         "--gpus", str(ranks), "--steps", "2", "--warmup", "1", "--pods-per-step", "300",
                         "--namespaces", "16", "--ref-events", "0", "--latency-seconds", "0.5",
                         "--sink-workers", "2", "--fixture-workers", "2", "--no-placement",
-                        "--decode-threads", "0"],
+                        "--decode-threads", "0", "--step-timeout", "45"],
                        capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -129,11 +129,11 @@ def test_bench_sharded_ranks_exactly_once(ranks):
     assert d["value"] > 0 and d["scaling"] == "weak"
     assert "namespace_scope=discover" in d["config"]["parallelism"]
     # every shard watched its own namespaces: 16 in total, split evenly, each event counted once
-    assert sum(p["scopes"] for p in d["per_rank"]) == 16
-    assert {p["scopes"] for p in d["per_rank"]} == {16 // ranks}
-    assert sum(p["events"] for p in d["per_rank"]) == 2 * ranks * 1500
+    assert sum(p["scopes"] for p in d["per_rank"]) == 16, d["per_rank"]
+    assert {p["scopes"] for p in d["per_rank"]} == {16 // ranks}, d["per_rank"]
+    assert sum(p["events"] for p in d["per_rank"]) == 2 * ranks * 1500, (d["per_rank"], r.stderr[-3000:])
     v = d["verify"]
-    assert v["exactly_once"] and v["duplicates"] == 0 and v["missing"] == 0, v
+    assert v["exactly_once"] and v["duplicates"] == 0 and v["missing"] == 0, (v, r.stderr[-3000:])
     assert v["expected"] == v["delivered_by_shards"] > 0
 
 
