@@ -1,7 +1,7 @@
 # k8s-watcher-amd — container image (SURVEY §2.2: the reference claims
 # "Dockerized" but ships no Dockerfile).
 FROM python:3.10-slim AS build
-RUN apt-get update && apt-get install -y --no-install-recommends g++ libssl-dev && rm -rf /var/lib/apt/lists/*
+RUN apt-get update && apt-get install -y --no-install-recommends g++ libssl-dev zlib1g-dev && rm -rf /var/lib/apt/lists/*
 WORKDIR /app
 COPY requirements.txt ./
 COPY k8s_watcher_amd/ k8s_watcher_amd/

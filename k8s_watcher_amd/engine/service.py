@@ -44,7 +44,7 @@ from ..parallel.spool import Spool, SpoolReplayer
 from ..utils.config import Settings
 from ..utils.fastlog import EventLog
 from ..utils.logsetup import SERVICE_LOGGER
-from .checkpoint import load_checkpoint, save_checkpoint
+from .checkpoint import load_checkpoint, native_snapshot, save_checkpoint, write_native
 from .namespaces import NamespaceWatcher
 from .pipeline import EventPipeline
 from .reflector import Reflector, WatchFailed
@@ -108,6 +108,7 @@ class WatcherService:
         self._failure: Optional[asyncio.Future] = None
         self._saved_rvs: Dict[str, Optional[str]] = {}
         self._multi = False  # several (or dynamic) watch scopes, each with its own pipeline
+        self.last_checkpoint: Optional[dict] = None
         self._live = False  # scopes follow namespace changes once start() has built the first set
 
     # ------------------------------------------------------------------ setup
@@ -263,12 +264,14 @@ class WatcherService:
                           f"(key={s.watcher.shard.key}); watch scopes: {[x or '*' for x in scopes]}")
         cache = make_pod_cache(self._native_pipeline())
         saved_rvs = {}
+        owed: list = []
         ck = s.watcher.checkpoint.path
         if ck:
             loaded = load_checkpoint(ck, native_cache=self._native_pipeline())
             if loaded is not None:
-                saved_rvs, cache, _ = loaded
-                self.log.info(f"Resuming from checkpoint {ck}: {len(cache)} cached pods")
+                saved_rvs, cache, _, owed = loaded
+                self.log.info(f"Resuming from checkpoint {ck}: {len(cache)} cached pods"
+                              + (f", {len(owed)} owed notifications" if owed else ""))
         self._saved_rvs = saved_rvs
         self.pipeline = EventPipeline(s, self.decoder, self.notifier, self.metrics, cache, self.event_log,
                                       event_sharding=self._event_sharding())
@@ -278,6 +281,10 @@ class WatcherService:
         if saved_rvs and None not in scopes:
             # pods of namespaces this shard no longer watches would never be reconciled
             self._forget_namespaces_except(set(scopes))
+        if owed:
+            # the checkpoint's cut: clusterapi never acknowledged these; send them
+            # (in their original order) before the watches resume after them
+            self._resubmit_owed(owed)
         self.metrics.gauges["cached_pods"] = lambda: float(len(cache))
         self.metrics.gauges["notify_outstanding"] = lambda: float(self.notifier.outstanding())
         self.metrics.gauges["watch_scopes"] = lambda: float(len(self.reflectors))
@@ -475,8 +482,8 @@ class WatcherService:
             if not drained and checkpoint and self.spool is not None:
                 await self.notifier.close()  # spools the rest
                 closed = drained = True
-        if checkpoint and drained:
-            await self._write_checkpoint()
+        if checkpoint and (drained or self._native_checkpoint()):
+            await self._write_checkpoint()  # format 2 carries whatever is still owed
         tasks = list(self._tasks) + list(self._scope_tasks.values())
         for t in tasks:
             if not t.done():
@@ -503,16 +510,64 @@ class WatcherService:
             await self.shutdown()
 
     # ------------------------------------------------------------------ checkpoint
+    def _native_checkpoint(self) -> bool:
+        """Format 2 (consistent cut, no pause/drain): native cache + native notifier core."""
+        return (self._native_pipeline() and self.pipeline is not None
+                and hasattr(self.pipeline.cache, "snapshot")
+                and (self.notifier is None or hasattr(self.notifier, "core") or not self.settings.clusterapi.enabled))
+
+    def _resubmit_owed(self, owed: list) -> None:
+        core = getattr(self.notifier, "core", None)
+        if core is None:
+            self.log.warning(f"{len(owed)} owed notifications in the checkpoint: no native notifier to resend them")
+            return
+        now = time.monotonic_ns()
+        for uid, etype, ns, name, body in owed:
+            core.submit_body(uid, etype, ns, name, body, now)
+        self.metrics.c["checkpoint_owed_resent"] += len(owed)
+        self.notifier.flush()
+
     async def _write_checkpoint(self) -> None:
         ck = self.settings.watcher.checkpoint.path
         if not ck or self.pipeline is None:
             return
         scopes = {r.scope: r.rv for r in self.reflectors}
-        save_checkpoint(ck, scopes, self.pipeline.cache, {"written_at": time.time()})
+        meta = {"written_at": time.time()}
+        if self._native_checkpoint():
+            snap = native_snapshot(self.pipeline.cache, getattr(self.notifier, "core", None))
+            await self._write_snapshot(snap, ck, scopes, meta)
+            return
+        save_checkpoint(ck, scopes, self.pipeline.cache, meta)
+        self.metrics.c["checkpoints_written"] += 1
+
+    async def _write_snapshot(self, snap, ck: str, scopes: dict, meta: dict) -> None:
+        st = snap.stats()
+        loop = asyncio.get_running_loop()
+        nbytes, secs = await loop.run_in_executor(None, write_native, snap, ck, scopes, meta)
+        g = self.metrics.gauges
+        last = {"checkpoint_stall_ms": st["snapshot_seconds"] * 1e3, "checkpoint_write_ms": secs * 1e3,
+                "checkpoint_bytes": float(nbytes), "checkpoint_pods": float(st["entries"]),
+                "checkpoint_owed": float(st["owed"]), "checkpoint_written_at": meta["written_at"]}
+        for k, v in last.items():
+            g[k] = (lambda v=v: v)
+        self.last_checkpoint = dict(last)
         self.metrics.c["checkpoints_written"] += 1
 
     async def checkpoint_now(self, drain_timeout: float = 30.0) -> bool:
-        """Quiescent checkpoint: pause readers, drain notifier, save, resume."""
+        """Write a checkpoint now.
+
+        Native engine + notifier core: a consistent cut taken synchronously on
+        the loop thread (``PodCache.snapshot``, a few ms per 100k pods) and
+        written on an executor thread — the watches keep running. Otherwise:
+        pause readers, drain the notifier, save, resume (format 1)."""
+        if self._native_checkpoint():
+            ck = self.settings.watcher.checkpoint.path
+            if not ck or self.pipeline is None:
+                return False
+            scopes = {r.scope: r.rv for r in self.reflectors}
+            snap = native_snapshot(self.pipeline.cache, getattr(self.notifier, "core", None))
+            await self._write_snapshot(snap, ck, scopes, {"written_at": time.time()})
+            return True
         for r in self.reflectors:
             r.set_paused(True)
         try:

@@ -19,6 +19,7 @@
 #include <Python.h>
 
 #include <arpa/inet.h>
+#include <fcntl.h>
 #include <openssl/err.h>
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
@@ -31,6 +32,7 @@
 #include <sys/syscall.h>
 #include <sys/types.h>
 #include <unistd.h>
+#include <zlib.h>
 
 #include <algorithm>
 #include <atomic>
@@ -1866,6 +1868,7 @@ PyObject* kw_bench_parse(PyObject*, PyObject* args) {
 #include "podcache.inc"
 #include "logsink.inc"
 #include "engine.inc"
+#include "checkpoint.inc"
 
 PyMethodDef module_methods[] = {
     {"bench_parse", (PyCFunction)kw_bench_parse, METH_VARARGS, "bench_parse(data, mode=2, repeat=1)"},
@@ -1902,7 +1905,8 @@ PyMODINIT_FUNC PyInit__kwcore(void) {
     if (PyType_Ready(&ScannerType) < 0) return nullptr;
     Py_INCREF(&ScannerType);
     PyModule_AddObject(m, "ResponseScanner", (PyObject*)&ScannerType);
-    if (register_engine(m) < 0 || register_podcache(m) < 0 || register_pipeline(m) < 0 || register_logsink(m) < 0)
+    if (register_engine(m) < 0 || register_podcache(m) < 0 || register_pipeline(m) < 0 || register_logsink(m) < 0 ||
+        register_checkpoint(m) < 0)
         return nullptr;
     const char* names[6] = {"ADDED", "MODIFIED", "DELETED", "BOOKMARK", "ERROR", "INVALID"};
     for (int i = 0; i < 6; ++i) {

@@ -46,7 +46,7 @@ def build_command(sanitize: str = "", out: str = SO) -> list:
     opt = ["-O1", "-g"] + SANITIZERS[sanitize] if sanitize else ["-O3"]
     return [compiler(), *opt, "-std=c++17", "-pthread", "-fPIC", "-shared", "-fvisibility=hidden",
             "-fno-strict-aliasing", "-Wall", "-Wno-shadow", "-Wno-unused-function", "-Wno-psabi",
-            f"-I{inc}", f"-I{os.path.dirname(SRC)}", SRC, "-o", out, "-lssl", "-lcrypto"]
+            f"-I{inc}", f"-I{os.path.dirname(SRC)}", SRC, "-o", out, "-lssl", "-lcrypto", "-lz"]
 
 
 def sanitizer_so(kind: str) -> str:

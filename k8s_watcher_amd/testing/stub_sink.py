@@ -207,8 +207,13 @@ class StubSink:
                 pass
 
 
+_GEN = b'"k8s-watcher.test/generation":"'
+
+
 def payload_key(body: bytes) -> bytes:
-    """``uid|event_type|phase`` of a payload without a JSON parse (soak verification).
+    """``uid|event_type|phase`` of a payload without a JSON parse (soak verification),
+    plus ``|<generation>`` when the pod carries the replay fixture's
+    ``k8s-watcher.test/generation`` annotation (steady pods MODIFIED every round).
 
     The first ``"uid":`` in a payload is the top-level one (``name`` and
     ``namespace`` precede it and are plain strings)."""
@@ -218,6 +223,10 @@ def payload_key(body: bytes) -> bytes:
     et = body[j:body.find(b'"', j)]
     k = body.find(b'"status":{"phase":') + 18
     phase = body[k:body.find(b",", k)].strip(b'"')
+    g = body.find(_GEN)
+    if g >= 0:
+        g += len(_GEN)
+        return b"|".join((uid, et, phase, body[g:body.find(b'"', g)]))
     return b"|".join((uid, et, phase))
 
 

@@ -55,9 +55,9 @@ def test_native_cache_checkpoint_round_trip(tmp_path):
     nat.observe("ADDED", "b", "2", None, None, None)
     path = str(tmp_path / "ck.json")
     save_checkpoint(path, {"*": "2"}, nat)
-    scopes, loaded, _ = load_checkpoint(path, native_cache=True)
+    scopes, loaded, _, _ = load_checkpoint(path, native_cache=True)
     assert scopes == {"*": "2"}
     assert type(loaded) is type(nat)
     assert snapshot(loaded) == snapshot(nat)
-    _, py, _ = load_checkpoint(path)
+    _, py, _, _ = load_checkpoint(path)
     assert snapshot(py) == snapshot(nat)

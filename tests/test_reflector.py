@@ -370,6 +370,49 @@ def test_checkpoint_restart_exactly_once(tmp_path):
     run(body())
 
 
+def test_native_checkpoint_carries_owed_notifications(tmp_path):
+    """Format 2 (native engine + notifier core) is a consistent cut taken
+    without pausing the watch or draining the notifier: notifications
+    clusterapi has not acknowledged are stored in the checkpoint and re-sent
+    first after a crash — none lost, none of the acknowledged ones repeated."""
+    ck = str(tmp_path / "ckpt.bin")
+
+    async def body():
+        ov = {"watcher": {"checkpoint": {"path": ck, "interval_seconds": 3600}},
+              "clusterapi": {"retry": {"delay_seconds": 30, "max_attempts": 5}}}
+        async with Stack(overrides=ov) as st:
+            f = st.factory
+            svc = st.service()
+            await svc.start()
+            acked = [st.srv.create(f.running(f.new_pod())) for _ in range(3)]
+            await st.settle(3)
+            st.sink.state.down = True  # clusterapi answers 503: the next ones stay owed (retry in 30 s)
+            owed = [st.srv.create(f.running(f.new_pod())) for _ in range(5)]
+            for _ in range(200):
+                if svc.metrics.c["notify_retried"] >= 5:
+                    break
+                await asyncio.sleep(0.01)
+            assert svc.notifier.outstanding() == 5
+            assert await svc.checkpoint_now()  # no drain: returns with 5 still owed
+            assert svc.last_checkpoint["checkpoint_owed"] == 5
+            assert svc.last_checkpoint["checkpoint_pods"] == 8
+            with open(ck, "rb") as fh:
+                assert fh.read(8) == b"KWCKPT02"
+            # crash: no final checkpoint, the owed requests die with the process
+            svc.stop()
+            await svc.shutdown(drain_timeout=0, checkpoint=False)
+            st.sink.state.down = False
+            svc2 = st.service()
+            await svc2.start()
+            await st.settle(8)
+            got = st.delivered()
+            assert sorted(u for u, _, _ in got) == sorted(p["metadata"]["uid"] for p in acked + owed)
+            assert svc2.metrics.c["checkpoint_owed_resent"] == 5
+            assert svc2.metrics.c["relists"] == 0  # resumed from the checkpointed RV
+
+    run(body())
+
+
 def test_checkpoint_restart_after_compaction_diffs(tmp_path):
     ck = str(tmp_path / "ckpt.json")
 
