@@ -1,0 +1,348 @@
+#!/usr/bin/env python3
+"""Long soak with memory accounting (BASELINE config #5: bookmark/resume across API-server restarts).
+
+    python -m benchmarks.soak --minutes 60 [--pods 10000] [--step-seconds 5] [--out f.json]
+
+A real watcher process (``main.py production --config-dir …``: critical
+filter, namespace filter, format-2 checkpoints every 5 s, ``/metrics``) runs
+for ``--minutes`` against ``testing/replay_server.py`` (``churn``: ``--pods``
+pod lifecycles = 5×pods events per step, one step every ``--step-seconds``)
+and the verify-mode stub clusterapi. The schedule mixes, per step:
+
+* normal steps;
+* every 7th: the API server drops every watch mid-step (restart): the watcher
+  must resume from its resourceVersion — every event exactly once;
+* every 11th: compaction mid-step (410): the watcher relists and diffs — the
+  intermediate events of that step are gone for good (what a real API server
+  does), but every pod's final state (DELETED) must arrive, once;
+* every 3rd: a BOOKMARK moves the resume point without events;
+* every ``--kill-every`` steps: SIGKILL of the watcher mid-step and a restart
+  from the checkpoint — nothing lost; duplicates allowed (re-sent owed
+  notifications and events since the checkpoint) and counted.
+
+Every ``--sample-seconds`` the harness records the watcher's RSS (VmRSS/VmHWM)
+and its gauges: cached pods and cache bytes, owed notifications and bytes,
+checkpoint stall. The sink's keys are handed over and reset every 50 steps
+(SIGUSR2) so neither side grows with the run; each step is judged once the
+window has passed it. Output: per-sample series + per-step verdicts + an RSS
+slope after warm-up (least squares, MiB/hour).
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import glob
+import json
+import os
+import shutil
+import signal
+import subprocess
+import sys
+import tempfile
+import textwrap
+import time
+from typing import Dict, List, Optional, Set, Tuple
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from benchmarks.restart_soak import free_port, scrape  # noqa: E402
+
+TARGETS = ("default", "production", "monitoring", "kube-system")  # config/production.yaml
+
+
+def vm(pid: int) -> Dict[str, float]:
+    out = {}
+    try:
+        with open(f"/proc/{pid}/status") as fh:
+            for line in fh:
+                if line.startswith(("VmRSS:", "VmHWM:")):
+                    out[line.split(":")[0]] = int(line.split()[1]) / 1024
+    except OSError:
+        pass
+    return out
+
+
+def slope_mib_per_hour(points: List[Tuple[float, float]]) -> Optional[float]:
+    if len(points) < 3:
+        return None
+    n = len(points)
+    mx = sum(t for t, _ in points) / n
+    my = sum(v for _, v in points) / n
+    sxx = sum((t - mx) ** 2 for t, _ in points)
+    if sxx == 0:
+        return None
+    return sum((t - mx) * (v - my) for t, v in points) / sxx * 3600
+
+
+class Soak:
+    def __init__(self, a) -> None:
+        self.a = a
+        self.dir = tempfile.mkdtemp(prefix="kw-soak-")
+        self.verify_dir = os.path.join(self.dir, "verify")
+        os.makedirs(self.verify_dir)
+        self.metrics_port = free_port()
+        self.sink_port = free_port()
+        self.samples: List[dict] = []
+        self.watcher: Optional[subprocess.Popen] = None
+        self.counts: Dict[int, Dict[str, int]] = {}  # step -> key -> deliveries
+        self.verdicts: List[dict] = []
+        self.kinds: Dict[int, str] = {}
+        self.kills = 0
+        self.t0 = time.monotonic()
+
+    # ------------------------------------------------------------------ fixtures
+    async def start(self) -> None:
+        from k8s_watcher_amd.testing.replay_server import Template
+        t = time.monotonic()
+        self.template = Template("churn", self.a.pods, 0)
+        # per event: (uid suffix, type, phase, ns) — what the production profile notifies
+        self.expect: List[Tuple[str, str, str, bool]] = []
+        import json as _json
+        for et, segs, uid in self.template.events:
+            obj = _json.loads(self.template.obj(segs, 0, uid, 0))
+            phase = (obj.get("status") or {}).get("phase") or ""
+            ns = obj["metadata"]["namespace"]
+            critical = et == "DELETED" or phase in ("Succeeded", "Failed")
+            self.expect.append((uid[8:], et, phase, critical and ns in TARGETS))
+        print(f"template: {len(self.expect)} events/step ({time.monotonic() - t:.1f}s)", file=sys.stderr, flush=True)
+        spawn = lambda *c: asyncio.create_subprocess_exec(  # noqa: E731
+            *c, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
+            stderr=asyncio.subprocess.DEVNULL, start_new_session=True, cwd=ROOT)
+        self.replay = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.replay_server",
+                                  "--template", "churn", "--pods", str(self.a.pods))
+        self.sink = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.stub_sink", "--port",
+                                str(self.sink_port), "--workers", str(self.a.sink_workers),
+                                "--verify-dir", self.verify_dir)
+        ready = (await asyncio.wait_for(self.replay.stdout.readline(), 900)).decode().split()
+        self.api_port, self.E = int(ready[1]), int(ready[2])
+        await self.sink.stdout.readline()
+        await asyncio.sleep(0.3)
+        cfg = os.path.join(self.dir, "config")
+        os.makedirs(cfg)
+        with open(os.path.join(self.dir, "kubeconfig"), "w") as fh:
+            fh.write(textwrap.dedent(f"""
+                current-context: c
+                clusters: [{{name: c, cluster: {{server: "http://127.0.0.1:{self.api_port}"}}}}]
+                contexts: [{{name: c, context: {{cluster: c, user: u}}}}]
+                users: [{{name: u, user: {{token: x}}}}]
+                """))
+        with open(os.path.join(cfg, "base.yaml"), "w") as fh:
+            fh.write(textwrap.dedent(f"""
+                kubernetes: {{config_file: {os.path.join(self.dir, "kubeconfig")}}}
+                clusterapi:
+                  health_check_on_start: false
+                  retry: {{max_attempts: 10, delay_seconds: 0.2}}
+                metrics: {{enabled: true, host: 127.0.0.1, port: {self.metrics_port}}}
+                watcher:
+                  retry: {{max_attempts: 0, delay_seconds: 0.1, max_delay_seconds: 2}}
+                  checkpoint: {{path: {os.path.join(self.dir, "state", "checkpoint.bin")}, interval_seconds: 5}}
+                """))
+        with open(os.path.join(cfg, "production.yaml"), "w") as fh:
+            fh.write(textwrap.dedent(f"""
+                environment: production
+                clusterapi: {{base_url: "http://127.0.0.1:{self.sink_port}", pool: {{connections: 4, pipeline_depth: 32}}}}
+                watcher:
+                  namespaces: [{", ".join(TARGETS)}]
+                  log_level: WARNING
+                  alerts: {{critical_events_only: true}}
+                """))
+        self.cfg = cfg
+
+    async def cmd(self, line: str) -> int:
+        self.replay.stdin.write((line + "\n").encode())
+        await self.replay.stdin.drain()
+        return int((await self.replay.stdout.readline()).decode().split()[2])
+
+    def start_watcher(self) -> None:
+        log = open(os.path.join(self.dir, "watcher.log"), "ab")
+        self.watcher = subprocess.Popen([sys.executable, os.path.join(ROOT, "main.py"), "production",
+                                         "--config-dir", self.cfg], cwd=ROOT, stdout=log, stderr=log,
+                                        start_new_session=True)
+
+    async def wait_watching(self) -> None:
+        for _ in range(6000):
+            if await self.cmd("WATCHERS") >= 1 and scrape(self.metrics_port).get("cached_pods") is not None:
+                return
+            await asyncio.sleep(0.01)
+        raise TimeoutError("watcher did not connect")
+
+    # ------------------------------------------------------------------ sampling
+    def sample(self, step: int) -> None:
+        m = scrape(self.metrics_port)
+        v = vm(self.watcher.pid)
+        s = {"t": round(time.monotonic() - self.t0, 1), "step": step, "rss_mb": v.get("VmRSS"),
+             "hwm_mb": v.get("VmHWM")}
+        for k in ("cached_pods", "cache_bytes", "notify_outstanding", "notify_outstanding_bytes",
+                  "checkpoint_stall_ms", "checkpoint_write_ms", "checkpoint_bytes", "events_received",
+                  "notify_delivered", "expired_410", "watch_restarts", "relists", "bookmarks"):
+            if k in m:
+                s[k] = m[k]
+        self.samples.append(s)
+
+    # ------------------------------------------------------------------ verification
+    def harvest(self, upto_step: int) -> None:
+        """Take the sink's keys (dump + reset) and judge every step < upto_step."""
+        for f in glob.glob(os.path.join(self.verify_dir, "sink-*.json")):
+            os.unlink(f)
+        os.killpg(self.sink.pid, signal.SIGUSR2)
+        deadline = time.monotonic() + 120
+        while len(glob.glob(os.path.join(self.verify_dir, "sink-*.json"))) < self.a.sink_workers:
+            if time.monotonic() > deadline:
+                break
+            time.sleep(0.05)
+        for f in glob.glob(os.path.join(self.verify_dir, "sink-*.json")):
+            with open(f) as fh:
+                for k, n in json.load(fh)["keys"].items():
+                    step = int(k[:8], 16)
+                    d = self.counts.setdefault(step, {})
+                    d[k] = d.get(k, 0) + n
+        for step in sorted(s for s in self.counts if s < upto_step):
+            self.judge(step, self.counts.pop(step))
+
+    def judge(self, step: int, got: Dict[str, int]) -> None:
+        kind = self.kinds.get(step, "normal")
+        prefix = f"{step & 0xFFFFFFFF:08x}"
+        want: Set[str] = {f"{prefix}{u}|{et}|{ph}" for u, et, ph, n in self.expect if n}
+        dups = sum(v - 1 for v in got.values() if v > 1)
+        if kind == "expire":
+            # the compacted window is gone for good (a pod born and deleted inside
+            # it is unobservable, as with a real API server); every pod that was
+            # notified at all must end DELETED — the relist diff sends it
+            seen = {k.split("|")[0] for k in got}
+            have_del = {k.split("|")[0] for k in got if "|DELETED|" in k}
+            missing = len(seen - have_del)
+            ok = missing == 0 and dups == 0
+        else:
+            missing = len(want - set(got))
+            ok = missing == 0 and (dups == 0 or kind in ("kill", "pre-kill"))
+        self.verdicts.append({"step": step, "kind": kind, "ok": ok, "missing": missing, "duplicates": dups,
+                              "received": sum(got.values())})
+
+    async def close(self) -> None:
+        if self.watcher is not None and self.watcher.poll() is None:
+            os.killpg(self.watcher.pid, signal.SIGTERM)
+            try:
+                self.watcher.wait(20)
+            except subprocess.TimeoutExpired:
+                os.killpg(self.watcher.pid, signal.SIGKILL)
+        for p in (self.replay, self.sink):
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except (ProcessLookupError, PermissionError):
+                pass
+            try:
+                await asyncio.wait_for(p.wait(), 10)
+            except asyncio.TimeoutError:
+                os.killpg(p.pid, signal.SIGKILL)
+            t = getattr(p, "_transport", None)
+            if t is not None:
+                t.close()
+        shutil.rmtree(self.dir, ignore_errors=True)
+
+
+async def amain(a) -> dict:
+    s = Soak(a)
+    try:
+        await s.start()
+        s.start_watcher()
+        await s.wait_watching()
+        await s.cmd("STEP 0")  # warm-up step, judged like the others
+        end = time.monotonic() + a.minutes * 60
+        step = 1
+        last_sample = 0.0
+        next_harvest = 50
+        events = s.E
+        while time.monotonic() < end:
+            t_step = time.monotonic()
+            half = s.E // 2
+            if a.kill_every and step % a.kill_every == 0:
+                s.kinds[step] = "kill"
+                # the last checkpoint (every 5 s) may predate these: re-sent after the restart
+                for back in range(1, int(5.0 / a.step_seconds) + 3):
+                    if s.kinds.get(step - back, "normal") == "normal":
+                        s.kinds[step - back] = "pre-kill"
+                send = asyncio.ensure_future(s.cmd(f"STEP {step}"))
+                await asyncio.sleep(a.step_seconds * 0.1)
+                s.sample(step)
+                os.killpg(s.watcher.pid, signal.SIGKILL)
+                s.watcher.wait()
+                s.kills += 1
+                s.start_watcher()
+                await send
+                await s.wait_watching()  # back before the next drop/compaction: a watcher that is
+                # down across a compaction legitimately never sees pods born and gone inside it
+            elif step % 11 == 0:
+                s.kinds[step] = "expire"
+                await s.cmd(f"STEP {step} expire={half}")
+            elif step % 7 == 0:
+                s.kinds[step] = "drop"
+                await s.cmd(f"STEP {step} drop={half}")
+            else:
+                await s.cmd(f"STEP {step}")
+            if step % 3 == 0:
+                await s.cmd("BOOKMARK")
+            events += s.E
+            while time.monotonic() < t_step + a.step_seconds:
+                if time.monotonic() - last_sample >= a.sample_seconds:
+                    last_sample = time.monotonic()
+                    s.sample(step)
+                    r = s.samples[-1]
+                    print(f"[{r['t']:7.1f}s] step {step} rss {r.get('rss_mb')} MiB cached {r.get('cached_pods')} "
+                          f"owed {r.get('notify_outstanding')} ({r.get('notify_outstanding_bytes')} B)",
+                          file=sys.stderr, flush=True)
+                await asyncio.sleep(0.05)
+            if step >= next_harvest:
+                s.harvest(step - 10)  # steps well behind the stream are complete
+                next_harvest = step + 50
+            step += 1
+        # let the stream finish, then judge everything
+        await asyncio.sleep(max(5.0, a.step_seconds))
+        s.sample(step)
+        s.harvest(step + 1)
+        after = [x for x in s.samples if x["t"] >= a.warmup_minutes * 60 and x.get("rss_mb")]
+        bad = [v for v in s.verdicts if not v["ok"]]
+        last = s.samples[-1]
+        summary = {
+            "minutes": a.minutes, "steps": step, "events_replayed": events, "pods_per_step": a.pods,
+            "watcher_kills": s.kills,
+            "steps_by_kind": {k: sum(1 for v in s.verdicts if v["kind"] == k)
+                              for k in ("normal", "drop", "expire", "kill", "pre-kill")},
+            "steps_failed": len(bad), "failed_examples": bad[:5],
+            "duplicates_outside_kill_steps": sum(v["duplicates"] for v in s.verdicts
+                                                 if v["kind"] not in ("kill", "pre-kill")),
+            "duplicates_in_kill_steps": sum(v["duplicates"] for v in s.verdicts if v["kind"] in ("kill", "pre-kill")),
+            "notifications_checked": sum(v["received"] for v in s.verdicts),
+            "rss_mb_after_warmup": {"min": min(x["rss_mb"] for x in after) if after else None,
+                                    "max": max(x["rss_mb"] for x in after) if after else None,
+                                    "slope_mib_per_hour": slope_mib_per_hour([(x["t"], x["rss_mb"]) for x in after])},
+            "peak_rss_mb_last_process": last.get("hwm_mb"),
+            "last_sample": last,
+        }
+        return {"summary": summary, "samples": s.samples, "verdicts": s.verdicts}
+    finally:
+        await s.close()
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--minutes", type=float, default=60)
+    ap.add_argument("--pods", type=int, default=10000)
+    ap.add_argument("--step-seconds", type=float, default=5.0)
+    ap.add_argument("--kill-every", type=int, default=60, help="SIGKILL the watcher every N steps (0 = never)")
+    ap.add_argument("--sample-seconds", type=float, default=10.0)
+    ap.add_argument("--warmup-minutes", type=float, default=5.0)
+    ap.add_argument("--sink-workers", type=int, default=2)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args(argv)
+    res = asyncio.run(amain(a))
+    print(json.dumps(res["summary"], indent=1))
+    if a.out:
+        with open(a.out, "w") as fh:
+            json.dump(res, fh, indent=1)
+    return 0 if res["summary"]["steps_failed"] == 0 else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

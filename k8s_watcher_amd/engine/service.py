@@ -286,7 +286,12 @@ class WatcherService:
             # (in their original order) before the watches resume after them
             self._resubmit_owed(owed)
         self.metrics.gauges["cached_pods"] = lambda: float(len(cache))
+        if hasattr(cache, "memory"):  # native cache: bytes held (cores + keys), for memory accounting
+            self.metrics.gauges["cache_bytes"] = lambda: float(sum(v for k, v in cache.memory().items()
+                                                                   if k.endswith("_bytes")))
         self.metrics.gauges["notify_outstanding"] = lambda: float(self.notifier.outstanding())
+        if hasattr(self.notifier, "outstanding_bytes"):
+            self.metrics.gauges["notify_outstanding_bytes"] = lambda: float(self.notifier.outstanding_bytes())
         self.metrics.gauges["watch_scopes"] = lambda: float(len(self.reflectors))
         self.log.info(f"Starting Pod watcher in {s.environment} environment...")
         if s.watcher.namespaces:

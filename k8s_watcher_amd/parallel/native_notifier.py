@@ -96,6 +96,8 @@ class NativeNotifierPool:
         self.addr = None
         self.high_water = settings.pool.queue_size
         self.low_water = max(1, settings.pool.queue_size // 2)
+        self.high_bytes = settings.pool.max_queued_bytes
+        self.low_bytes = settings.pool.max_queued_bytes // 2
         self.saturated = False
         self.on_saturation = on_saturation
         self.closing = False
@@ -150,6 +152,9 @@ class NativeNotifierPool:
 
     def outstanding(self) -> int:
         return self.core.pending()
+
+    def outstanding_bytes(self) -> int:
+        return self.core.pending_bytes()
 
     async def health_check(self, timeout: float = 5.0) -> bool:
         client = HttpClient(self.settings.base_url, self._health_ssl_context(), timeout=timeout)
@@ -332,13 +337,14 @@ class NativeNotifierPool:
                 self.writers.add(i)
                 self.loop.add_writer(sock.fileno(), self._writable, i)
         pending = self.core.pending()
-        if not self.saturated and pending >= self.high_water:
+        pbytes = self.core.pending_bytes()
+        if not self.saturated and (pending >= self.high_water or pbytes >= self.high_bytes):
             self.saturated = True
             if self.threaded:  # the I/O thread wakes us when the queue has drained enough
-                self.core.signal_below(self.low_water)
+                self.core.signal_below(self.low_water, self.low_bytes)
             if self.on_saturation:
                 self.on_saturation(True)
-        elif self.saturated and pending <= self.low_water:
+        elif self.saturated and pending <= self.low_water and pbytes <= self.low_bytes:
             self.saturated = False
             if self.on_saturation:
                 self.on_saturation(False)

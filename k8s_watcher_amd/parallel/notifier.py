@@ -250,8 +250,11 @@ class NotifierPool:
         self.unsent: Dict[str, NotifyRequest] = {}
         self.seq = 0
         self.pending = 0
+        self.pending_bytes = 0
         self.high_water = settings.pool.queue_size
         self.low_water = max(1, settings.pool.queue_size // 2)
+        self.high_bytes = settings.pool.max_queued_bytes
+        self.low_bytes = settings.pool.max_queued_bytes // 2
         self.saturated = False
         self.on_saturation = on_saturation
         self.closing = False
@@ -300,7 +303,7 @@ class NotifierPool:
             conn.queue.append(req)
             self._dirty.append(conn)
             self.metrics.c["notify_submitted"] += 1
-            self._add_pending(1)
+            self._add_pending(1, len(r.body))
             n += 1
         return n
 
@@ -313,7 +316,7 @@ class NotifierPool:
     def _finish(self, req: NotifyRequest) -> None:
         if self.replaying:
             self.replaying.pop(req.seq, None)
-        self._add_pending(-1)
+        self._add_pending(-1, -len(req.body))
 
     # ------------------------------------------------------------------ public API
     def submit(self, uid: str, etype: str, ns: Optional[str], name: Optional[str], core: bytes,
@@ -327,6 +330,7 @@ class NotifierPool:
         if self.settings.pool.coalesce:
             old = self.unsent.get(uid)
             if old is not None:
+                self._add_pending(0, len(body) - len(old.body))
                 old.body = body
                 old.etype = etype
                 self.seq += 1
@@ -343,7 +347,7 @@ class NotifierPool:
         conn.queue.append(req)
         if len(conn.queue) == 1 or conn.state != _Conn.UP:
             self._dirty.append(conn)
-        self._add_pending(1)
+        self._add_pending(1, len(body))
 
     def _take_token(self, conn: "_Conn") -> bool:
         now = time.monotonic()
@@ -440,18 +444,22 @@ class NotifierPool:
     def outstanding(self) -> int:
         return self.pending
 
+    def outstanding_bytes(self) -> int:
+        return self.pending_bytes
+
     # ------------------------------------------------------------------ bookkeeping
-    def _add_pending(self, n: int) -> None:
+    def _add_pending(self, n: int, nbytes: int = 0) -> None:
         self.pending += n
+        self.pending_bytes += nbytes
         if self.pending > 0:
             self._idle_event.clear()
         else:
             self._idle_event.set()
-        if not self.saturated and self.pending >= self.high_water:
+        if not self.saturated and (self.pending >= self.high_water or self.pending_bytes >= self.high_bytes):
             self.saturated = True
             if self.on_saturation:
                 self.on_saturation(True)
-        elif self.saturated and self.pending <= self.low_water:
+        elif self.saturated and self.pending <= self.low_water and self.pending_bytes <= self.low_bytes:
             self.saturated = False
             if self.on_saturation:
                 self.on_saturation(False)

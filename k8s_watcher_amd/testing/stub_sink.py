@@ -248,7 +248,7 @@ def run_sink_process(port: int, workers: int = 1, latency: float = 0.0,
 
     With ``verify_dir`` every worker records ``uid|event_type|phase`` counts and
     writes them to ``verify_dir/sink-<pid>.json`` on SIGTERM (and, without
-    stopping, on SIGUSR1).
+    stopping, on SIGUSR1; SIGUSR2 also clears them after the dump).
     """
     import signal as _signal
     pids = []
@@ -282,6 +282,12 @@ def run_sink_process(port: int, workers: int = 1, latency: float = 0.0,
         loop.add_signal_handler(_signal.SIGTERM, stop.set)
         if verify_dir:
             loop.add_signal_handler(_signal.SIGUSR1, dump)  # a snapshot while still serving
+
+            def dump_and_reset() -> None:  # long soaks: hand the keys over, keep memory flat
+                dump()
+                sink.state.keys.clear()
+                sink.state.count = 0
+            loop.add_signal_handler(_signal.SIGUSR2, dump_and_reset)
         await stop.wait()
         if verify_dir:
             dump()

@@ -210,6 +210,7 @@ class NotifierPoolSettings:
     connections: int = 16
     pipeline_depth: int = 8
     queue_size: int = 65536
+    max_queued_bytes: int = 64 << 20  # backpressure also past this many owed body bytes
     coalesce: bool = False
     native: bool = True  # C++ notifier core (watcher.engine: native)
     io_thread: bool = False  # native core serves its sockets on a dedicated thread (profiles/notifier_io_thread_gpu_box.md)
@@ -487,6 +488,8 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
             connections=max(1, _as_int(pool.get("connections", 16), "clusterapi.pool.connections")),
             pipeline_depth=max(1, _as_int(pool.get("pipeline_depth", 8), "clusterapi.pool.pipeline_depth")),
             queue_size=max(1, _as_int(pool.get("queue_size", 65536), "clusterapi.pool.queue_size")),
+            max_queued_bytes=max(1 << 16, _as_int(pool.get("max_queued_bytes", 64 << 20),
+                                                  "clusterapi.pool.max_queued_bytes")),
             coalesce=_as_bool(pool.get("coalesce", False), "clusterapi.pool.coalesce"),
             native=_as_bool(pool.get("native", True), "clusterapi.pool.native"),
             io_thread=_as_bool(pool.get("io_thread", False), "clusterapi.pool.io_thread"),

@@ -20,7 +20,8 @@ TS = "2025-01-01T00:00:00.000001"
 
 def settings(url, **kw):
     pool = NotifierPoolSettings(connections=kw.pop("connections", 4), pipeline_depth=kw.pop("depth", 1),
-                                queue_size=kw.pop("queue_size", 1000), coalesce=kw.pop("coalesce", False))
+                                queue_size=kw.pop("queue_size", 1000), coalesce=kw.pop("coalesce", False),
+                                max_queued_bytes=kw.pop("max_bytes", 64 << 20))
     retry = RetryPolicy(kw.pop("attempts", 3), kw.pop("delay", 0.01), 2.0, 1.0, 0.0)
     return ClusterApiSettings(base_url=url, pool=pool, retry=retry, **kw)
 
@@ -258,6 +259,33 @@ def test_backpressure_signals(pool_cls):
         pool.flush()
         assert pool.saturated
         await pool.drain(10)
+        await close(sink, pool)
+
+    run(body())
+    assert flips == [True, False]
+
+
+def test_backpressure_by_bytes(pool_cls):
+    """clusterapi.pool.max_queued_bytes: few but large notifications (pods
+    with big annotations) saturate the pool by bytes long before queue_size;
+    it releases once both counts are back under half."""
+    flips = []
+
+    async def body():
+        sink = StubSink(latency=0.05)
+        await sink.start()
+        pool = pool_cls(settings(sink.url, queue_size=10_000, connections=2, max_bytes=1 << 16), Metrics(),
+                        on_saturation=flips.append)
+        big = build_core({"metadata": {"name": "p", "namespace": "default", "uid": "u",
+                                       "annotations": {"blob": "x" * 20_000}}, "status": {"phase": "Running"}},
+                         "production")
+        for i in range(5):  # 5 x ~20 KB > 64 KiB, 5 << queue_size
+            pool.submit(f"u{i}", "ADDED", "default", "p", big, 0, TS)
+        pool.flush()
+        assert pool.saturated and pool.outstanding() == 5
+        assert pool.outstanding_bytes() >= 5 * 20_000
+        await pool.drain(10)
+        assert pool.outstanding_bytes() == 0
         await close(sink, pool)
 
     run(body())
