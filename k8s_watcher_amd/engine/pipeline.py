@@ -109,8 +109,8 @@ class EventPipeline:
                 elog.log(level, msg)
         if submits:
             submit = self.notifier.submit
-            for uid, et, ns, name, core in submits:
-                submit(uid, et, ns, name, core, read_ns, ts)
+            for uid, et, ns, name, core, ev_ts in submits:
+                submit(uid, et, ns, name, core, read_ns, ev_ts)
         self.notifier.flush()
         elog.flush()
         return ctrl
@@ -130,7 +130,6 @@ class EventPipeline:
         decoder = self.decoder
         submit = self.notifier.submit
         shard = self.shard if self.shard.active else None
-        ts = None
         for ev in events:
             et = ev[E_TYPE]
             if et not in _POD_EVENTS:
@@ -173,9 +172,8 @@ class EventPipeline:
                 core = decoder.core(ev)
             if et != DELETED:
                 set_core(uid, core)
-            if ts is None:
-                ts = event_timestamp(self.ts_mode)
-            submit(uid, et, ns, name, core, read_ns, ts)
+            # stamped per event as it is submitted (reference: at payload build, pod_watcher.py:199)
+            submit(uid, et, ns, name, core, read_ns, event_timestamp(self.ts_mode))
         self.notifier.flush()
         elog.flush()
         return ctrl

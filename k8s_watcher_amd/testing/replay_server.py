@@ -134,6 +134,8 @@ class ReplayServer:
         # live objects: uid -> (step, event index | -1 for the initial state)
         self.live: Dict[str, Tuple[int, int]] = {}
         self._pending: List[List[int]] = []  # [step, start, stop) ranges sent but not yet applied to live
+        self._lists: Dict[str, Tuple[int, List[bytes], int]] = {}  # continue token -> (rv, items, offset)
+        self._list_seq = 0
         if template.kind == "steady":
             self.live = {uid: (-1, j) for j, (_, uid) in enumerate(template.initial)}
         # Whole steps rendered ahead of time into memory files so that, during
@@ -183,7 +185,7 @@ class ReplayServer:
             else:
                 self.live[u] = (step, i)
 
-    def list_body(self) -> bytes:
+    def _live_items(self) -> List[bytes]:
         self._materialize()
         items = []
         t = self.t
@@ -194,8 +196,29 @@ class ReplayServer:
             else:
                 _, segs, _ = t.events[i]
                 items.append(t.obj(segs, RV0 + step * self.E + i, u, step))
-        return (b'{"kind":"PodList","apiVersion":"v1","metadata":{"resourceVersion":"%d"},"items":[%s]}'
-                % (self.rv, b",".join(items)))
+        return items
+
+    def list_body(self, limit: int = 0, cont: Optional[str] = None) -> bytes:
+        """A PodList; with ``limit`` paginated like kube-apiserver: every page of
+        one LIST comes from the snapshot taken for its first page (same RV),
+        linked by an opaque ``continue`` token."""
+        if cont:
+            snap = self._lists.get(cont)
+            if snap is None:
+                return b""  # unknown/expired token: the caller answers 410
+            rv, items, off = snap
+            del self._lists[cont]
+        else:
+            rv, items, off = self.rv, self._live_items(), 0
+        end = len(items) if not limit else min(len(items), off + limit)
+        meta = b'"resourceVersion":"%d"' % rv
+        if end < len(items):
+            self._list_seq += 1
+            token = f"r{self._list_seq}"
+            self._lists[token] = (rv, items, end)
+            meta += b',"continue":"%s","remainingItemCount":%d' % (token.encode(), len(items) - end)
+        return (b'{"kind":"PodList","apiVersion":"v1","metadata":{%s},"items":[%s]}'
+                % (meta, b",".join(items[off:end])))
 
     def backlog(self, since: int) -> bytes:
         """Every event with resourceVersion in (since, self.rv]."""
@@ -231,7 +254,15 @@ class ReplayServer:
                     body = json.dumps({"kind": "NamespaceList", "apiVersion": "v1", "metadata": {},
                                        "items": [{"metadata": {"name": "default"}}]}).encode()
                 else:
-                    body = self.list_body()
+                    body = self.list_body(int(q.get("limit") or 0), q.get("continue"))
+                    if not body:
+                        body = json.dumps({"kind": "Status", "apiVersion": "v1", "status": "Failure",
+                                           "reason": "Expired", "code": 410,
+                                           "message": "The provided continue parameter is too old"}).encode()
+                        writer.write(b"HTTP/1.1 410 Gone\r\nContent-Type: application/json\r\n"
+                                     b"Content-Length: %d\r\n\r\n" % len(body) + body)
+                        await writer.drain()
+                        continue
                 writer.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n"
                              % len(body) + body)
                 await writer.drain()
