@@ -399,11 +399,20 @@ async def rank_main(args, d: Dist) -> dict:
         metrics.latency.reset()
         d.barrier()
         n0, s0 = c["events_received"], c["notify_delivered"]
+        prof = None
+        if os.environ.get("BENCH_PROFILE") and d.rank == 0:  # cProfile of the timed steps only
+            import cProfile
+            prof = cProfile.Profile()
         cpu0 = cpu_snapshot(fx)
         t0 = time.perf_counter()
+        if prof is not None:
+            prof.enable()
         for k in range(args.warmup, args.warmup + args.steps):
             await run_step(k, per_step)
         elapsed = time.perf_counter() - t0
+        if prof is not None:
+            prof.disable()
+            prof.dump_stats(os.environ["BENCH_PROFILE"])
         cpu1 = cpu_snapshot(fx)
         events = c["events_received"] - n0
         notified = c["notify_delivered"] - s0
