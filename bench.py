@@ -35,7 +35,9 @@ scale-out, weak scaling):
 barriers; the slowest rank's clock is used and ``value`` is the events of all
 ranks over it. Then the latency phase paces ``--latency-rate`` ev/s per rank
 (config #4's 100 ev/s) for ``--latency-seconds``: p50/p99 of socket read of the
-watch chunk → 2xx from clusterapi, over the samples of every rank. Last, the
+watch chunk → 2xx from clusterapi, over the samples of every rank; then again at
+``--latency-rate-high`` (1,000 ev/s) for ``--latency-seconds-high``, which gives
+>= 5,000 notified samples in the production profile (``latency_high_rate``). Last, the
 sink's counts prove the union of the shards delivered every notifiable event
 exactly once (``verify``: no event missing, none twice, none by two shards).
 
@@ -99,6 +101,9 @@ def parse_args(argv=None):
                     help="sink does not count payload keys (no exactly-once proof)")
     ap.add_argument("--latency-rate", type=float, default=100.0, help="ev/s per rank in the latency phase")
     ap.add_argument("--latency-seconds", type=float, default=30.0)
+    ap.add_argument("--latency-rate-high", type=float, default=1000.0,
+                    help="second latency phase, ev/s per rank (0: skip)")
+    ap.add_argument("--latency-seconds-high", type=float, default=30.0)
     ap.add_argument("--ref-events", type=int, default=10000,
                     help="events for the reference-equivalent run (0 = skip, vs_baseline null)")
     ap.add_argument("--step-timeout", type=float, default=300.0)
@@ -426,6 +431,16 @@ async def rank_main(args, d: Dist) -> dict:
         await run_latency(fx, d, svc, c, k_lat, args.latency_rate * d.world, count, args.step_timeout,
                           notifiable)
         lat = list(metrics.latency.samples or [])
+        # and at 10x that, long enough for >= 5,000 notified samples in the 20%-notifying profile
+        lat_hi = []
+        if args.latency_rate_high > 0 and args.latency_seconds_high > 0:
+            metrics.latency.reset()
+            k_lat += 1
+            count = max(1, int(args.latency_rate_high * d.world * args.latency_seconds_high))
+            count = min(count, shared["events_per_step"])
+            await run_latency(fx, d, svc, c, k_lat, args.latency_rate_high * d.world, count, args.step_timeout,
+                              notifiable)
+            lat_hi = list(metrics.latency.samples or [])
         failed = c["notify_failed"]
         delivered_total = c["notify_delivered"]
         svc.stop()
@@ -440,7 +455,7 @@ async def rank_main(args, d: Dist) -> dict:
                 ref = await run_reference(args, fx, shared, targets, k_lat + 1)
         return {"elapsed": elapsed, "events": events, "notified": notified,
                 "events_per_step": shared["events_per_step"], "per_step_mine": per_step, "scopes": len(mine),
-                "lat": lat, "sat": sat, "failed": failed, "ref": ref, "verify": verify,
+                "lat": lat, "lat_hi": lat_hi, "sat": sat, "failed": failed, "ref": ref, "verify": verify,
                 "delivered_total": delivered_total, "notifiable": notifiable[0],
                 "fixture_workers": shared["fixture_workers"], "sink_workers": getattr(fx, "sink_workers", None),
                 "cpu_util": {k: round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0
@@ -561,6 +576,7 @@ def main(argv=None) -> int:
     notified = d.reduce(float(res["notified"]), "SUM")
     delivered_total = d.reduce(float(res["delivered_total"]), "SUM")
     lat = [x for r in d.all_gather(res["lat"]) for x in r]
+    lat_hi = [x for r in d.all_gather(res["lat_hi"]) for x in r]
     sat = [x for r in d.all_gather(res["sat"]) for x in r]
     per_rank = d.all_gather({"events": res["events"], "scopes": res["scopes"], "elapsed": round(res["elapsed"], 4),
                              "notified": res["notified"]})
@@ -609,6 +625,9 @@ def main(argv=None) -> int:
         "p99_latency_ms": round(p99 / 1e6, 3) if p99 else None,
         "latency_rate_ev_s_per_rank": args.latency_rate,
         "latency_samples": len(lat),
+        "latency_high_rate": ({"rate_ev_s_per_rank": args.latency_rate_high, "samples": len(lat_hi),
+                               "p50_ms": round(pct(lat_hi, 50) / 1e6, 3), "p90_ms": round(pct(lat_hi, 90) / 1e6, 3),
+                               "p99_ms": round(pct(lat_hi, 99) / 1e6, 3)} if lat_hi else None),
         "notified_per_s": round(notified / elapsed, 1),
         "notify_failed": res["failed"],
         "verify": verify,

@@ -32,7 +32,7 @@ def test_smoke_end_to_end():
 
 def test_bench_line_is_valid():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
-                          "--pods-per-step", "1000", "--ref-events", "500", "--latency-seconds", "1"],
+                          "--pods-per-step", "1000", "--ref-events", "500", "--latency-seconds", "1", "--latency-seconds-high", "1"],
                          capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
     line = json.loads(out.stdout.strip().splitlines()[-1])
@@ -45,7 +45,7 @@ def test_bench_line_is_valid():
 def test_tls_bench_line_is_valid():
     """production.yaml's https clusterapi through the native TLS notifier core, on the host."""
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
-                          "--pods-per-step", "1000", "--ref-events", "0", "--latency-seconds", "1", "--tls"],
+                          "--pods-per-step", "1000", "--ref-events", "0", "--latency-seconds", "1", "--latency-rate-high", "0", "--tls"],
                          capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
     line = json.loads(out.stdout.strip().splitlines()[-1])

@@ -117,7 +117,7 @@ def test_bench_sharded_ranks_exactly_once(ranks):
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
                         "--gpus", str(ranks), "--steps", "2", "--warmup", "1", "--pods-per-step", "300",
-                        "--namespaces", "16", "--ref-events", "0", "--latency-seconds", "0.5",
+                        "--namespaces", "16", "--ref-events", "0", "--latency-seconds", "0.5", "--latency-seconds-high", "0.5",
                         "--sink-workers", "2", "--fixture-workers", "2", "--no-placement",
                         "--decode-threads", "0", "--step-timeout", "45"],
                        capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
@@ -140,7 +140,7 @@ def test_bench_sharded_ranks_exactly_once(ranks):
 def test_bench_single_rank_cluster_watch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
                         "--pods-per-step", "300", "--namespaces", "8", "--ref-events", "200",
-                        "--latency-seconds", "0.5", "--sink-workers", "1", "--no-placement"],
+                        "--latency-seconds", "0.5", "--latency-seconds-high", "0.5", "--sink-workers", "1", "--no-placement"],
                        capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
