@@ -381,17 +381,24 @@ async def rank_main(args, d: Dist) -> dict:
         decode_threads = native_pl.decode_threads() if native_pl is not None else None
         debug = bool(os.environ.get("BENCH_DEBUG"))
         notifiable = [0]
+        # cumulative target, not "received at step start + expect": rank 0 may
+        # leave the barrier and start step k+1 before a slower rank has looked
+        # at its counter, so some of step k+1's events can already be counted
+        target = [c["events_received"]]
 
         async def run_step(k: int, expect: int, pace: str = "") -> None:
-            base = c["events_received"]
+            base = target[0]
+            target[0] += expect
             t_start = time.perf_counter()
             sent = asyncio.ensure_future(fx.cmd(f"PACE {k} {pace}" if pace else f"STEP {k}")) \
                 if d.rank == 0 else None
             deadline = time.monotonic() + args.step_timeout
-            while c["events_received"] < base + expect or svc.notifier.outstanding() > 0:
+            while c["events_received"] < target[0] or svc.notifier.outstanding() > 0:
                 if time.monotonic() > deadline:
                     raise TimeoutError(f"rank {d.rank} step {k}: {c['events_received'] - base}/{expect} events, "
-                                       f"{svc.notifier.outstanding()} notifications outstanding")
+                                       f"{svc.notifier.outstanding()} notifications outstanding; streams "
+                                       f"{[(r.scope, r.watch_count, r.rv) for r in svc.reflectors]}; "
+                                       f"counters { {n: v for n, v in c.items() if v and 'latency' not in n} }")
                 await asyncio.sleep(0.0005)
             if sent is not None:
                 notifiable[0] += int((await sent)[3])
