@@ -90,6 +90,9 @@ def parse_args(argv=None):
     ap.add_argument("--watch-read-bytes", type=int, default=None, help="watcher.watch_read_bytes")
     ap.add_argument("--no-placement", dest="placement", action="store_false",
                     help="no per-rank L3 domain assignment (each watcher still pins per watcher.decode_affinity)")
+    ap.add_argument("--fixture-placement", default="apart", choices=["apart", "inherit"],
+                    help="apart: the API-server fixture and the sink run on L3 domains no watcher rank holds "
+                         "(as remote servers would); inherit: on rank 0's watcher domain (round-1 behaviour)")
     ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
     ap.add_argument("--io-thread", action="store_true",
                     help="serve the C++ notifier core's sockets on its own thread (clusterapi.pool.io_thread)")
@@ -107,6 +110,8 @@ def parse_args(argv=None):
     ap.add_argument("--ref-events", type=int, default=10000,
                     help="events for the reference-equivalent run (0 = skip, vs_baseline null)")
     ap.add_argument("--step-timeout", type=float, default=300.0)
+    ap.add_argument("--probe", action="store_true",
+                    help="time the event-loop thread's native calls (split / decode wait / apply / notifier I/O)")
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
     return ap.parse_args(argv)
 
@@ -172,10 +177,30 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-async def spawn(*cmd: str):
+async def spawn(*cmd: str, cpus=None):
     return await asyncio.create_subprocess_exec(
         *cmd, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
-        stderr=asyncio.subprocess.DEVNULL, start_new_session=True, cwd=ROOT)
+        stderr=asyncio.subprocess.DEVNULL, start_new_session=True, cwd=ROOT,
+        preexec_fn=(lambda: os.sched_setaffinity(0, cpus)) if cpus else None)
+
+
+def fixture_cpus(all_cpus: set, watcher_domains: list) -> "set | None":
+    """CPUs for the fixture processes: the L3 domains no watcher rank holds,
+    on rank 0's package first (its memory traffic stays on one socket), so the
+    mock API server and sink neither share cores nor last-level cache with a
+    watcher — a real API server and clusterapi are other machines. None when
+    nothing is left (small hosts): they then share whatever the OS gives them."""
+    from k8s_watcher_amd.utils.cpus import l3_domains, package_of
+    held = set().union(*watcher_domains) if watcher_domains else set()
+    if not held:
+        return None
+    free = [dom for dom in l3_domains() if not (dom & held) and dom <= all_cpus]
+    if not free:
+        rest = all_cpus - held
+        return rest or None
+    pkg = package_of(min(watcher_domains[0]))
+    same = [dom for dom in free if package_of(min(dom)) == pkg]
+    return set().union(*(same or free))
 
 
 def cpu_ranges(cpus) -> "str | None":
@@ -227,12 +252,13 @@ class Fixtures:
         self.verify_dir = None
         self.pki = None
 
-    async def start(self, args, world: int, names, targets) -> dict:
+    async def start(self, args, world: int, names, targets, cpus=None) -> dict:
         fw = args.fixture_workers or max(2, 2 * world)
+        self.cpus = cpus
         self.replay = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.cluster_replay",
                                   "--pods", str(args.pods_per_step * world),
                                   "--namespace-list", ",".join(names), "--targets", ",".join(targets),
-                                  "--workers", str(fw))
+                                  "--workers", str(fw), cpus=cpus)
         sink_port = free_port()
         tls_args = []
         if args.tls:
@@ -245,7 +271,7 @@ class Fixtures:
             self.verify_dir = tempfile.mkdtemp(prefix="bench-verify-")
             verify = ["--verify-dir", self.verify_dir]
         self.sink = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.stub_sink", "--port", str(sink_port),
-                                "--workers", str(self.sink_workers), *tls_args, *verify)
+                                "--workers", str(self.sink_workers), *tls_args, *verify, cpus=cpus)
         line = (await asyncio.wait_for(self.replay.stdout.readline(), 600)).decode()
         assert line.startswith("READY "), line
         self.info = json.loads(line[6:])
@@ -324,12 +350,19 @@ async def rank_main(args, d: Dist) -> dict:
     scope = args.watch_scope if args.watch_scope != "auto" else ("cluster" if d.world == 1 else "discover")
     names = namespace_names(args.namespaces)
     targets = target_namespaces(args.targets, names)
+    all_cpus = os.sched_getaffinity(0)
     watcher_cpus = placement(d) if args.placement else None
     if watcher_cpus:
         os.sched_setaffinity(0, watcher_cpus)  # the decode workers inherit it
+    held = [set(x) for x in d.all_gather(sorted(watcher_cpus) if watcher_cpus else []) if x]
+    fx_cpus = None
+    if args.fixture_placement == "apart":
+        # without this the fixtures inherit rank 0's pinning: the replay and
+        # sink workers would run on the watcher's own cores and L3
+        fx_cpus = fixture_cpus(all_cpus, held) if held else all_cpus
     fx = Fixtures()
     try:
-        shared = await fx.start(args, d.world, names, targets) if d.rank == 0 else None
+        shared = await fx.start(args, d.world, names, targets, fx_cpus) if d.rank == 0 else None
         shared = d.broadcast(shared)
         log_path = os.path.join("/tmp", f"k8s-watcher-bench-{os.getpid()}.log")
         setup_logging(args.profile, "WARNING" if args.profile == "production" else "INFO", log_file=log_path)
@@ -385,6 +418,7 @@ async def rank_main(args, d: Dist) -> dict:
         # leave the barrier and start step k+1 before a slower rank has looked
         # at its counter, so some of step k+1's events can already be counted
         target = [c["events_received"]]
+        phases: list = []
 
         async def run_step(k: int, expect: int, pace: str = "") -> None:
             base = target[0]
@@ -393,15 +427,27 @@ async def rank_main(args, d: Dist) -> dict:
             sent = asyncio.ensure_future(fx.cmd(f"PACE {k} {pace}" if pace else f"STEP {k}")) \
                 if d.rank == 0 else None
             deadline = time.monotonic() + args.step_timeout
+            t_first = t_all = t_sent = None
             while c["events_received"] < target[0] or svc.notifier.outstanding() > 0:
+                if t_first is None and c["events_received"] > base:
+                    t_first = time.perf_counter()
+                if t_all is None and c["events_received"] >= target[0]:
+                    t_all = time.perf_counter()
+                if t_sent is None and sent is not None and sent.done():
+                    t_sent = time.perf_counter()
                 if time.monotonic() > deadline:
                     raise TimeoutError(f"rank {d.rank} step {k}: {c['events_received'] - base}/{expect} events, "
                                        f"{svc.notifier.outstanding()} notifications outstanding; streams "
                                        f"{[(r.scope, r.watch_count, r.rv) for r in svc.reflectors]}; "
                                        f"counters { {n: v for n, v in c.items() if v and 'latency' not in n} }")
                 await asyncio.sleep(0.0005)
+            t_end = time.perf_counter()
             if sent is not None:
                 notifiable[0] += int((await sent)[3])
+            # where a step's time goes (rank 0): fixture send done, first and
+            # last event in, every notification acknowledged
+            phases.append({"first_event": (t_first or t_end) - t_start, "fixture_sent": (t_sent or t_end) - t_start,
+                           "all_events": (t_all or t_end) - t_start, "drained": t_end - t_start})
             if debug:
                 print(f"rank {d.rank} step {k}: {time.perf_counter() - t_start:.3f}s", file=sys.stderr)
             await d.abarrier()
@@ -415,17 +461,28 @@ async def rank_main(args, d: Dist) -> dict:
         if os.environ.get("BENCH_PROFILE") and d.rank == 0:  # cProfile of the timed steps only
             import cProfile
             prof = cProfile.Profile()
+        kw = None
+        if args.probe:
+            from k8s_watcher_amd.ops import native as _native
+            kw = _native.load()
+            kw.probe(True)
         cpu0 = cpu_snapshot(fx)
         t0 = time.perf_counter()
         if prof is not None:
             prof.enable()
+        phases.clear()
         for k in range(args.warmup, args.warmup + args.steps):
             await run_step(k, per_step)
         elapsed = time.perf_counter() - t0
+        step_phases = {key: round(sum(p[key] for p in phases) / len(phases) * 1000, 2) for key in phases[0]} \
+            if phases else None
         if prof is not None:
             prof.disable()
             prof.dump_stats(os.environ["BENCH_PROFILE"])
         cpu1 = cpu_snapshot(fx)
+        probe = kw.probe(False) if kw is not None else None
+        if probe:
+            probe["loop_cpu_ns"] = int((cpu1["thread_loop"] - cpu0["thread_loop"]) * 1e9)
         events = c["events_received"] - n0
         notified = c["notify_delivered"] - s0
         sat = list(metrics.latency.samples or [])
@@ -470,8 +527,9 @@ async def rank_main(args, d: Dist) -> dict:
                 "cpu_threads": sorted((round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0
                                        if k.startswith("thread_") and k != "thread_loop" and k in cpu1),
                                       reverse=True)[:8],
-                "decode_threads": decode_threads, "scope": scope,
-                "placement": {"watcher": cpu_ranges(watcher_cpus)}}
+                "decode_threads": decode_threads, "scope": scope, "step_phases_ms": step_phases, "probe": probe,
+                "placement": {"watcher": cpu_ranges(watcher_cpus), "fixtures": cpu_ranges(fx_cpus)
+                              if args.fixture_placement == "apart" else "inherit"}}
     finally:
         await fx.close()
 
@@ -642,6 +700,8 @@ def main(argv=None) -> int:
         "fixture_workers": res["fixture_workers"],
         "sink_workers": res["sink_workers"],
         "cpu_util_rank0": res["cpu_util"],
+        "step_phases_ms_rank0": res["step_phases_ms"],
+        **({"loop_probe_rank0": res["probe"]} if res["probe"] else {}),
         "cpu_other_threads_rank0": res["cpu_threads"],
         # the watcher's own efficiency (the rate is bound by the replay fixture's core when it hits 1.0)
         "events_per_watcher_cpu_second": (round(res["events"] / (res["cpu_util"]["watcher"] * res["elapsed"]), 1)

@@ -389,6 +389,7 @@ class _ClientProtocol(asyncio.BufferedProtocol):
                 self.transport.close()
 
     def connection_lost(self, exc) -> None:  # type: ignore[override]
+        self._rbuf = None  # up to watch_read_bytes (4 MiB) per connection
         try:
             self.parser.feed_eof()
         except Exception as err:  # noqa: BLE001
@@ -510,6 +511,10 @@ class HttpClient:
             raise HttpError(f"connect to {self.host}:{self.port} failed: {exc}") from None
         tune_socket(transport.get_extra_info("socket"), self.keepalive)
         self._all.append(proto)
+        # a closed connection leaves the client's books, whoever closed it (a
+        # watch ending, the server hanging up an idle keep-alive socket): every
+        # watch reconnect used to leave its protocol — and read buffer — here
+        proto.closed.add_done_callback(lambda _f, p=proto: self._forget(p))
         return proto
 
     async def _acquire(self, timeout: float) -> _ClientProtocol:
@@ -528,10 +533,11 @@ class HttpClient:
             self._forget(proto)
 
     def _forget(self, proto: _ClientProtocol) -> None:
-        try:
-            self._all.remove(proto)
-        except ValueError:
-            pass
+        for group in (self._all, self._idle):
+            try:
+                group.remove(proto)
+            except ValueError:
+                pass
 
     # ------------------------------------------------------------------ API
     async def request(self, method: str, path: str, query: Optional[Dict[str, object]] = None,

@@ -1875,6 +1875,7 @@ PyMethodDef module_methods[] = {
     {"event_timestamp", (PyCFunction)kw_event_timestamp, METH_O, "event_timestamp(utc) -> str"},
     {"cpu_features", (PyCFunction)kw_cpu_features, METH_NOARGS, "SIMD paths in use"},
     {"set_simd", (PyCFunction)kw_set_simd, METH_O, "enable/disable the AVX2 scanner"},
+    {"probe", (PyCFunction)kw_probe, METH_O, "probe(enable) -> event-loop thread time in native calls since the last call"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef moddef = {PyModuleDef_HEAD_INIT, "_kwcore", "native watch-event decoder", -1, module_methods};

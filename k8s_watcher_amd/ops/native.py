@@ -44,7 +44,7 @@ SANITIZERS = {
 def build_command(sanitize: str = "", out: str = SO) -> list:
     inc = sysconfig.get_paths()["include"]
     opt = ["-O1", "-g"] + SANITIZERS[sanitize] if sanitize else ["-O3"]
-    return [compiler(), *opt, "-std=c++17", "-pthread", "-fPIC", "-shared", "-fvisibility=hidden",
+    return [compiler(), *opt, "-std=c++20", "-pthread", "-fPIC", "-shared", "-fvisibility=hidden",
             "-fno-strict-aliasing", "-Wall", "-Wno-shadow", "-Wno-unused-function", "-Wno-psabi",
             f"-I{inc}", f"-I{os.path.dirname(SRC)}", SRC, "-o", out, "-lssl", "-lcrypto", "-lz"]
 

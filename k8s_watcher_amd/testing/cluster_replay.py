@@ -181,8 +181,10 @@ class ScopeStream:
                  uid_off: np.ndarray, gidx: np.ndarray, E: int) -> None:
         self.scope, self.base, self.ev_off, self.rv_off = scope, base, ev_off, rv_off
         self.uid_off, self.gidx, self.E = uid_off, gidx, E
-        self.buf: Optional[np.ndarray] = None  # patched in place per step (render)
+        self.buf: Optional[np.ndarray] = None  # patched in place per step (render / ensure)
         self.buf_step = -1
+        self._rv_done = 0  # fields of buf_step patched so far (indices into rv_off / uid_off)
+        self._uid_done = 0
 
     @staticmethod
     def _patch(buf: np.ndarray, rv_off: np.ndarray, rvs: np.ndarray, uid_off: np.ndarray, step: int) -> None:
@@ -195,11 +197,25 @@ class ScopeStream:
 
     def render(self, step: int) -> memoryview:
         """The whole step: the scope's one buffer, its fixed-width fields set for ``step``."""
+        self.ensure(step, len(self.base))
+        return memoryview(self.buf)
+
+    def ensure(self, step: int, end: int) -> memoryview:
+        """Set ``step``'s fields in the bytes before ``end`` (a field that starts
+        there is set whole). Sending a step patches each slice just before it
+        is written, so the first bytes leave at once instead of after a pass
+        over the whole buffer, and patching overlaps the kernel's copies."""
         if self.buf is None:
             self.buf = self.base.copy()
         if self.buf_step != step:
-            self._patch(self.buf, self.rv_off, RV0 + step * self.E + self.gidx, self.uid_off, step)
-            self.buf_step = step
+            self.buf_step, self._rv_done, self._uid_done = step, 0, 0
+        j1 = int(np.searchsorted(self.rv_off, end))
+        u1 = int(np.searchsorted(self.uid_off, end))
+        if j1 > self._rv_done or u1 > self._uid_done:
+            j0, u0 = self._rv_done, self._uid_done
+            self._patch(self.buf, self.rv_off[j0:j1], RV0 + step * self.E + self.gidx[j0:j1],
+                        self.uid_off[u0:u1], step)
+            self._rv_done, self._uid_done = j1, u1
         return memoryview(self.buf)
 
     def event_bytes(self, step: int, j: int) -> bytes:
@@ -343,12 +359,15 @@ class Worker:
         for n in sorted({s for s, _ in self._targets()}):
             self.scope(n).render(k0)
 
-    async def _send(self, w: asyncio.StreamWriter, view: memoryview) -> None:
-        """Write ``view`` in slices, waiting for the socket between them: the
-        transport copies at most one slice, and the scope's buffer is free to
-        be patched again once every connection's send has returned."""
+    async def _send(self, w: asyncio.StreamWriter, sc: ScopeStream, k: int) -> None:
+        """Write step ``k`` of ``sc`` in slices, each patched just before it
+        goes out, waiting for the socket between them: the transport copies at
+        most one slice, and the scope's buffer is free to be patched again once
+        every connection's send has returned."""
         try:
-            for i in range(0, len(view), self.slice):
+            n = len(sc.base)
+            for i in range(0, n, self.slice):
+                view = sc.ensure(k, min(n, i + self.slice))
                 w.write(view[i:i + self.slice])
                 await w.drain()
         except (ConnectionError, RuntimeError):
@@ -357,8 +376,7 @@ class Worker:
     async def step(self, k: int) -> None:
         targets = self._targets()
         self._advance(k, 0, self.m.E)  # before the first await: a watch joining now gets it as backlog
-        views = {n: self.scope(n).render(k) for n in {s for s, _ in targets}}
-        await asyncio.gather(*(self._send(w, views[n]) for n, w in targets))
+        await asyncio.gather(*(self._send(w, self.scope(n), k) for n, w in targets))
 
     async def pace(self, k: int, rate: float, count: int, tick: float = 0.0005) -> None:
         """The first ``count`` events of step ``k`` at ``rate`` ev/s over the whole

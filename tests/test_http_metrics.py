@@ -113,3 +113,40 @@ def test_metrics_server_endpoints():
     assert "k8s_watcher_cached_pods 3.0" in metrics
     assert 'k8s_watcher_notify_latency_seconds_bucket{le="+Inf"} 1' in metrics
     assert (r0, r1, h, nf) == (503, 200, 200, 404)
+
+
+def test_closed_streams_leave_the_client():
+    """Every watch reconnect used to leave its protocol (and its read buffer,
+    up to watcher.watch_read_bytes = 4 MiB) in HttpClient._all: a slow leak
+    per reconnect that the long soak exposed. Closed connections, stream or
+    pooled, must drop out of the client's books and free their buffer."""
+    import asyncio
+
+    async def body():
+        async def handle(reader, writer):
+            await reader.readuntil(b"\r\n\r\n")
+            writer.write(b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n5\r\nhello\r\n")
+            await writer.drain()
+            await reader.read()  # until the client hangs up
+            writer.close()
+
+        srv = await asyncio.start_server(handle, "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        c = HttpClient(f"http://127.0.0.1:{port}")
+        got, protos = [], []
+        for _ in range(5):
+            stream, err = await c.stream("GET", "/watch", lambda d, _ns: got.append(bytes(d)),
+                                         read_size=4 << 20, zero_copy=True)
+            assert err is None
+            protos.append(stream._proto)
+            stream.close()
+            await asyncio.wait_for(stream.finished, 5)
+        await asyncio.sleep(0)
+        left = len(c._all)
+        await c.close()
+        srv.close()
+        return got, left, [p._rbuf for p in protos]
+
+    got, left, bufs = run(body())
+    assert len(got) == 5 and left == 0
+    assert all(b is None for b in bufs)
