@@ -90,9 +90,11 @@ def parse_args(argv=None):
     ap.add_argument("--watch-read-bytes", type=int, default=None, help="watcher.watch_read_bytes")
     ap.add_argument("--no-placement", dest="placement", action="store_false",
                     help="no per-rank L3 domain assignment (each watcher still pins per watcher.decode_affinity)")
-    ap.add_argument("--fixture-placement", default="apart", choices=["apart", "inherit"],
-                    help="apart: the API-server fixture and the sink run on L3 domains no watcher rank holds "
-                         "(as remote servers would); inherit: on rank 0's watcher domain (round-1 behaviour)")
+    ap.add_argument("--fixture-placement", default="inherit", choices=["apart", "inherit"],
+                    help="inherit: the API-server fixture and the sink share rank 0's L3 domain, so the watch "
+                         "bytes reach the watcher through that cache (as a NIC's DMA into the LLC would); apart: "
+                         "L3 domains no watcher holds — measured 35-40%% slower on the MI355X host "
+                         "(profiles/fixture_placement_gpu_box.md): every socket copy crosses dies")
     ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
     ap.add_argument("--io-thread", action="store_true",
                     help="serve the C++ notifier core's sockets on its own thread (clusterapi.pool.io_thread)")
@@ -357,8 +359,7 @@ async def rank_main(args, d: Dist) -> dict:
     held = [set(x) for x in d.all_gather(sorted(watcher_cpus) if watcher_cpus else []) if x]
     fx_cpus = None
     if args.fixture_placement == "apart":
-        # without this the fixtures inherit rank 0's pinning: the replay and
-        # sink workers would run on the watcher's own cores and L3
+        # by default the fixtures inherit rank 0's pinning (its cores and L3)
         fx_cpus = fixture_cpus(all_cpus, held) if held else all_cpus
     fx = Fixtures()
     try:
