@@ -88,6 +88,8 @@ def parse_args(argv=None):
     ap.add_argument("--decode-threads", default=None, help="watcher.decode_threads (int or auto)")
     ap.add_argument("--decode-affinity", default=None, choices=["auto", "none", "l3"])
     ap.add_argument("--watch-read-bytes", type=int, default=None, help="watcher.watch_read_bytes")
+    ap.add_argument("--watch-reader", default=None, choices=["native", "asyncio"], help="watcher.watch_reader")
+    ap.add_argument("--thread-pinning", default=None, choices=["auto", "none"], help="watcher.thread_pinning")
     ap.add_argument("--no-placement", dest="placement", action="store_false",
                     help="no per-rank L3 domain assignment (each watcher still pins per watcher.decode_affinity)")
     ap.add_argument("--fixture-placement", default="inherit", choices=["apart", "inherit"],
@@ -361,6 +363,11 @@ async def rank_main(args, d: Dist) -> dict:
     if args.fixture_placement == "apart":
         # by default the fixtures inherit rank 0's pinning (its cores and L3)
         fx_cpus = fixture_cpus(all_cpus, held) if held else all_cpus
+    elif watcher_cpus and args.thread_pinning != "none":
+        # ... minus the physical core watcher.thread_pinning gives the event-loop thread
+        from k8s_watcher_amd.utils.cpus import loop_core_split
+        split = loop_core_split(watcher_cpus)
+        fx_cpus = split[1] if split else None
     fx = Fixtures()
     try:
         shared = await fx.start(args, d.world, names, targets, fx_cpus) if d.rank == 0 else None
@@ -377,6 +384,8 @@ async def rank_main(args, d: Dist) -> dict:
                         "shard": {"count": d.world, "index": d.rank, "assignment": args.assignment},
                         **({"decode_threads": args.decode_threads} if args.decode_threads is not None else {}),
                         **({"watch_read_bytes": args.watch_read_bytes} if args.watch_read_bytes else {}),
+                        **({"watch_reader": args.watch_reader} if args.watch_reader else {}),
+                        **({"thread_pinning": args.thread_pinning} if args.thread_pinning else {}),
                         # placement already pinned this thread (the decode workers inherit it)
                         **({"decode_affinity": args.decode_affinity or ("none" if watcher_cpus else "auto")})},
         }
@@ -529,8 +538,8 @@ async def rank_main(args, d: Dist) -> dict:
                                        if k.startswith("thread_") and k != "thread_loop" and k in cpu1),
                                       reverse=True)[:8],
                 "decode_threads": decode_threads, "scope": scope, "step_phases_ms": step_phases, "probe": probe,
-                "placement": {"watcher": cpu_ranges(watcher_cpus), "fixtures": cpu_ranges(fx_cpus)
-                              if args.fixture_placement == "apart" else "inherit"}}
+                "placement": {"watcher": cpu_ranges(watcher_cpus), "fixtures": cpu_ranges(fx_cpus),
+                              "threads": svc.thread_placement}}
     finally:
         await fx.close()
 

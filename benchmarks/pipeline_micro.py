@@ -35,18 +35,34 @@ def unframe(data: bytes) -> bytes:
 
 
 def pipeline_rate(mod, data: bytes, n: int, threads: int, critical: bool, reps: int,
-                  read_size: int = READ_SIZE) -> float:
+                  read_size: int = READ_SIZE, notify: bool = False, probe: dict = None) -> float:
+    """``notify``: the production wiring — namespace filter over half the
+    namespaces and a native notifier core (never connected: submits queue up,
+    which is the apply-side cost of a notification)."""
     chunks = [data[j:j + read_size] for j in range(0, len(data), read_size)]
     best = float("inf")
     for _ in range(reps):
-        pl = mod.Pipeline("production", mod.PodCache(), {}, None, critical, False, 1, 0, True, True, None,
+        nsset = notifier = None
+        if notify:
+            nsset = frozenset(["default", "kube-system", "production", "monitoring"])
+            notifier = mod.Notifier(b"POST /x HTTP/1.1\r\nContent-Length: ", 4, 32, 3, 1.0, 2.0, 30.0,
+                                    False, False, [502, 503], {})
+        pl = mod.Pipeline("production", mod.PodCache(), {}, nsset, critical, False, 1, 0, True, True, notifier,
                           False, False, threads)
         spent = 0
+        if probe is not None:
+            mod.probe(True)
         for ch in chunks:
             hot = bytearray(ch)  # like a recv buffer: just written, in cache
             t0 = time.perf_counter_ns()
             pl.feed_chunked(hot, 0)
             spent += time.perf_counter_ns() - t0
+        if probe is not None:
+            got = mod.probe(False)
+            if spent < best:
+                probe.clear()
+                probe.update({k: round(got[k] / max(1, got["lines"]), 1)
+                              for k in ("split_ns", "wait_ns", "apply_ns", "run_ns")})
         best = min(best, spent)
         del pl
     return n / (best / 1e9)
@@ -76,17 +92,24 @@ def main(argv=None) -> int:
     mod.set_simd(True)
     res["simd"] = mod.cpu_features()
     for th in [int(x) for x in args.threads.split(",")]:
-        for critical, profile in ((True, "production (critical filter)"), (False, "all events notified")):
-            rate = pipeline_rate(mod, data, n, th, critical, args.reps, args.read_size)
-            res["pipeline"].append({"decode_threads": th, "profile": profile, "events_per_s": round(rate)})
+        for critical, notify, profile in ((True, False, "production (critical filter)"),
+                                          (False, False, "all events notified"),
+                                          (True, True, "production + ns filter + native notifier")):
+            pr = {}
+            rate = pipeline_rate(mod, data, n, th, critical, args.reps, args.read_size, notify, pr)
+            res["pipeline"].append({"decode_threads": th, "profile": profile, "events_per_s": round(rate),
+                                    "loop_ns_per_event": pr})
     print(f"# native pipeline ceiling, {n} events x {res['bytes_per_event']} B, SIMD {res['simd']}\n")
     print("| SIMD | skip | light extract | full extract | + payload core |  (ns/event, one thread)")
     print("|---|---|---|---|---|")
     for name, row in res["stages_ns_per_event"].items():
         print(f"| {name} | {row['skip']} | {row['light']} | {row['extract']} | {row['extract+core']} |")
-    print("\n| decode threads | profile | events/s |\n|---|---|---|")
+    print("\n| decode threads | profile | events/s | calling thread ns/event: split / decode wait / apply |"
+          "\n|---|---|---|---|")
     for r in res["pipeline"]:
-        print(f"| {r['decode_threads']} | {r['profile']} | {r['events_per_s']:,} |")
+        p = r["loop_ns_per_event"]
+        print(f"| {r['decode_threads']} | {r['profile']} | {r['events_per_s']:,} | "
+              f"{p.get('split_ns')} / {p.get('wait_ns')} / {p.get('apply_ns')} |")
     if args.json:
         with open(args.json, "w") as fh:
             json.dump(res, fh, indent=1)

@@ -94,11 +94,8 @@ class Reflector:
     def set_paused(self, paused: bool) -> None:
         self._paused = paused
         s = self.stream
-        if s is not None and s._proto.transport is not None:
-            if paused:
-                s._proto.transport.pause_reading()
-            else:
-                s._proto.transport.resume_reading()
+        if s is not None:
+            s._proto.set_reading(not paused)
 
     # ------------------------------------------------------------------ list
     async def relist(self, notify: bool = True) -> None:

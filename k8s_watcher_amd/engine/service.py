@@ -94,6 +94,9 @@ class WatcherService:
         self.notifier = None
         self.pipeline: Optional[EventPipeline] = None
         self._decode_pool = None
+        self._reader_hub = None
+        self.thread_placement = None
+        self._loop_affinity = None
         self.reflectors: List[Reflector] = []
         self.decoder = None
         self._stop = asyncio.Event()
@@ -278,6 +281,13 @@ class WatcherService:
         if self._native_pipeline():
             self._decode_pool = self._make_decode_pool()
             self.pipeline.attach_native(self._decode_pool)
+            if s.watcher.watch_reader == "native" and self.api.http.ssl_context is None:
+                # plain-TCP watches: socket reads on a native thread (net/reader.py)
+                from ..net.reader import WatchReaderHub
+                self._reader_hub = WatchReaderHub(s.watcher.watch_read_bytes or (4 << 20),
+                                                  s.watcher.watch_reader_buffers)
+                self.api.http.reader_hub = self._reader_hub
+            self._pin_threads()
         if saved_rvs and None not in scopes:
             # pods of namespaces this shard no longer watches would never be reconciled
             self._forget_namespaces_except(set(scopes))
@@ -417,6 +427,35 @@ class WatcherService:
                 self.log.info(f"Decode pool pinned to L3 domain CPUs {sorted(dom)}")
         return load().DecodePool(n) if n > 0 else 0
 
+    def _pin_threads(self) -> None:
+        """``watcher.thread_pinning: auto``: the event-loop thread (which applies
+        every event in stream order, the rate's bound) on a physical core of its
+        own; decode workers and the reader thread on the rest of the L3 domain."""
+        if self.settings.watcher.thread_pinning != "auto":
+            return
+        from ..utils.cpus import loop_core_split
+        try:
+            split = loop_core_split(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            return
+        if split is None:
+            return
+        loop_cpus, rest = split
+        tids = list(self._decode_pool.thread_ids()) if self._decode_pool else []
+        if self._reader_hub is not None:
+            tids.append(self._reader_hub.core.thread_id())
+        try:
+            for tid in tids:
+                if tid:
+                    os.sched_setaffinity(tid, rest)
+            self._loop_affinity = os.sched_getaffinity(0)  # restored at shutdown
+            os.sched_setaffinity(0, loop_cpus)  # this (the loop) thread; threads it starts later inherit it
+        except OSError as exc:
+            self.log.warning(f"Thread pinning skipped: {exc}")
+            return
+        self.thread_placement = {"loop": sorted(loop_cpus), "workers": sorted(rest)}
+        self.log.info(f"Event-loop thread pinned to CPUs {sorted(loop_cpus)}; {len(tids)} worker threads to the rest")
+
     def _native_pipeline(self) -> bool:
         w = self.settings.watcher
         return w.engine == "native" and w.state_format == "structured"
@@ -504,6 +543,17 @@ class WatcherService:
             await self.notifier.close()  # with a spool, whatever is still owed is written to it
         if self.spool is not None:
             self.spool.close()
+        if self._reader_hub is not None:
+            if self.api is not None:
+                self.api.http.reader_hub = None
+            self._reader_hub.close()
+            self._reader_hub = None
+        if self._loop_affinity is not None:
+            try:
+                os.sched_setaffinity(0, self._loop_affinity)
+            except OSError:
+                pass
+            self._loop_affinity = None
         if self.api is not None:
             await self.api.close()
 

@@ -345,6 +345,8 @@ class _ClientProtocol(asyncio.BufferedProtocol):
         self.stream_head: Optional[asyncio.Future] = None
         self.last_activity = time.monotonic()
         self.read_stamp = 0
+        self.hub = None  # net/reader.WatchReaderHub that reads this socket, once adopted
+        self.hub_sid = 0
 
     def deliver(self, data: bytes) -> None:
         """``parser.on_body`` for streams: body bytes + the socket-read timestamp."""
@@ -388,7 +390,44 @@ class _ClientProtocol(asyncio.BufferedProtocol):
             if self.transport is not None:
                 self.transport.close()
 
+    # net/reader.WatchReaderHub callbacks (event-loop thread)
+    def hub_data(self, view: memoryview, read_ns: int) -> None:
+        self.read_stamp = read_ns
+        self.last_activity = time.monotonic()
+        p = self.parser
+        try:
+            if p.state == ResponseParser.RAW and not p.buf and p.on_body is not None:
+                p.on_body(view)
+            else:
+                p.feed(bytes(view))
+        except Exception as exc:  # noqa: BLE001
+            self._fail(exc)
+            self.close()
+
+    def hub_eof(self, err: int) -> None:
+        """The hub saw the peer close (err 0) or the socket fail: end the
+        connection through the transport, as a read of EOF would."""
+        self._unhub()
+        if self.transport is not None:
+            self.transport.close()
+
+    def _unhub(self) -> None:
+        hub, self.hub = self.hub, None
+        if hub is not None:
+            hub.forget(self.hub_sid)
+
+    def set_reading(self, on: bool) -> None:
+        """Flow control for whoever reads the socket (the hub or asyncio)."""
+        if self.hub is not None:
+            self.hub.pause(self.hub_sid, not on)
+        elif self.transport is not None and not self.transport.is_closing():
+            if on:
+                self.transport.resume_reading()
+            else:
+                self.transport.pause_reading()
+
     def connection_lost(self, exc) -> None:  # type: ignore[override]
+        self._unhub()
         self._rbuf = None  # up to watch_read_bytes (4 MiB) per connection
         try:
             self.parser.feed_eof()
@@ -409,6 +448,7 @@ class _ClientProtocol(asyncio.BufferedProtocol):
                 and not self.busy and self.parser.keep_alive)
 
     def close(self) -> None:
+        self._unhub()  # the hub's dup of the socket goes first, or the peer never sees the close
         if self.transport is not None:
             self.transport.close()
 
@@ -476,6 +516,9 @@ class HttpClient:
         self.timeout = timeout
         self.max_idle = max_idle
         self.keepalive = keepalive  # TCP keep-alive / user timeout, seconds (net/sockopt.py)
+        # net/reader.WatchReaderHub: zero-copy raw streams on plain TCP are read
+        # by its native thread once their response head is in (None: asyncio)
+        self.reader_hub = None
         self._idle: List[_ClientProtocol] = []
         self._all: List[_ClientProtocol] = []
 
@@ -659,6 +702,10 @@ class HttpClient:
             proto.close()
             self._forget(proto)
             return sr, b"".join(err_parts)
+        hub = self.reader_hub
+        if (hub is not None and zero_copy and parser.state == ResponseParser.RAW and self.ssl_context is None
+                and not proto.closed.done()):
+            hub.adopt(proto)
         return sr, None
 
     async def close(self) -> None:

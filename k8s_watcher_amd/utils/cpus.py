@@ -216,3 +216,43 @@ def assign_domains(wanted: List[int], doms: List[frozenset]) -> List[int]:
         taken.add(choice)
         out.append(choice)
     return out
+
+
+def core_siblings(cpu: int, root: str = "") -> set:
+    """The hardware threads of ``cpu``'s physical core (itself without SMT)."""
+    try:
+        with open(f"{root}/sys/devices/system/cpu/cpu{cpu}/topology/thread_siblings_list") as fh:
+            return _parse_cpu_list(fh.read()) or {cpu}
+    except (OSError, ValueError):
+        return {cpu}
+
+
+def loop_core_split(cpus: set, min_cores: int = 4, root: str = "") -> Optional[tuple]:
+    """``(loop_cpus, other_cpus)`` for ``watcher.thread_pinning``: the lowest
+    physical core of ``cpus`` (both hardware threads) for the event-loop
+    thread, the rest for the decode workers, the reader thread — and, in the
+    benchmark, the fixtures. The loop thread applies every event in stream
+    order and bounds the rate; sharing its core with a busy SMT sibling cost
+    up to a third of its speed on the MI355X host (profiles/thread_pinning_gpu_box.md).
+    None when ``cpus`` lies in several L3 domains or has fewer than
+    ``min_cores`` physical cores (nothing to gain, or too little to spare)."""
+    if not cpus:
+        return None
+    first = min(cpus)
+    try:
+        with open(f"{root}/sys/devices/system/cpu/cpu{first}/cache/index3/shared_cpu_list") as fh:
+            if not cpus <= _parse_cpu_list(fh.read()):
+                return None
+    except (OSError, ValueError):
+        return None
+    cores, seen = [], set()
+    for c in sorted(cpus):
+        if c in seen:
+            continue
+        sib = core_siblings(c, root) & cpus
+        seen |= sib | {c}
+        cores.append(sib or {c})
+    if len(cores) < min_cores:
+        return None
+    loop = cores[0]
+    return set(loop), set(cpus) - loop

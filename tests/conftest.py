@@ -24,3 +24,21 @@ def _native_extension():
 
 def run(coro, timeout=60):
     return asyncio.run(asyncio.wait_for(coro, timeout))
+
+
+@pytest.fixture(autouse=True)
+def _keep_cpu_affinity():
+    """A test that starts a WatcherService without shutting it down must not
+    leave the test runner's thread pinned (watcher.thread_pinning / decode_affinity)."""
+    import os
+    try:
+        before = os.sched_getaffinity(0)
+    except (AttributeError, OSError):
+        yield
+        return
+    yield
+    try:
+        if os.sched_getaffinity(0) != before:
+            os.sched_setaffinity(0, before)
+    except OSError:
+        pass

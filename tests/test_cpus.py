@@ -48,3 +48,18 @@ def test_current_domain_is_allowed():
     if dom is not None:
         assert dom <= os.sched_getaffinity(0)
     assert all(d for d in cpus.l3_domains())
+
+
+def test_loop_core_split(tmp_path):
+    """8 cores x 2 threads in one L3 (CPUs n and n+8 are siblings): the loop
+    thread gets core 0 (CPUs 0 and 8), everything else goes to the workers.
+    Fewer than 4 cores, or CPUs from two L3 domains: no split."""
+    from k8s_watcher_amd.utils.cpus import loop_core_split
+    for c in range(16):
+        write(tmp_path, f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list", "0-15")
+        write(tmp_path, f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list", f"{c % 8},{c % 8 + 8}")
+    loop, rest = loop_core_split(set(range(16)), root=str(tmp_path))
+    assert loop == {0, 8} and rest == set(range(1, 8)) | set(range(9, 16))
+    assert loop_core_split({0, 1, 8, 9}, root=str(tmp_path)) is None  # 2 cores
+    write(tmp_path, "/sys/devices/system/cpu/cpu16/cache/index3/shared_cpu_list", "16-31")
+    assert loop_core_split(set(range(17)), root=str(tmp_path)) is None  # spans two L3 domains

@@ -1,0 +1,203 @@
+"""Native watch reader (``_kwcore.ReaderHub`` + ``net/reader.WatchReaderHub``).
+
+The hub must deliver every byte of every adopted stream, in order per stream,
+signal end of stream, stop reading a paused stream (TCP flow control does the
+rest), and leave the asyncio transport in charge of the connection's life.
+"""
+
+import asyncio
+import os
+import socket
+import time
+
+import pytest
+
+from conftest import run
+from k8s_watcher_amd.net.http import HttpClient
+from k8s_watcher_amd.net.reader import WatchReaderHub
+from k8s_watcher_amd.ops.native import load
+
+
+def _drain(core, want_bytes, timeout=5.0):
+    got, ends = {}, []
+    deadline = time.monotonic() + timeout
+    while sum(len(v) for v in got.values()) < want_bytes or (want_bytes == 0 and not ends):
+        if time.monotonic() > deadline:
+            break
+        for sid, buf, view, read_ns, err in core.take():
+            if view is not None:
+                assert read_ns > 0
+                got.setdefault(sid, bytearray()).extend(view)
+                view.release()
+                core.release(buf)
+            else:
+                ends.append((sid, err))
+        time.sleep(0.001)
+    return got, ends
+
+
+def test_hub_reads_streams_in_order_and_signals_eof():
+    mod = load()
+    core = mod.ReaderHub(64 * 1024, 4)
+    pairs = [socket.socketpair() for _ in range(3)]
+    sids = [core.add(os.dup(b.fileno())) for a, b in pairs]
+    payload = {sid: os.urandom(300_000) for sid in sids}  # several buffers each
+    for (a, _b), sid in zip(pairs, sids):
+        a.setblocking(True)
+    import threading
+
+    def send(a, data):
+        a.sendall(data)
+        a.shutdown(socket.SHUT_WR)
+
+    ths = [threading.Thread(target=send, args=(a, payload[sid])) for (a, _b), sid in zip(pairs, sids)]
+    for t in ths:
+        t.start()
+    got, ends = _drain(core, sum(len(v) for v in payload.values()))
+    for t in ths:
+        t.join()
+    deadline = time.monotonic() + 5
+    while len(ends) < 3 and time.monotonic() < deadline:
+        ends += [(sid, err) for sid, buf, view, _ns, err in core.take() if view is None]
+        time.sleep(0.001)
+    assert {sid: bytes(v) for sid, v in got.items()} == payload
+    assert sorted(ends) == sorted((sid, 0) for sid in sids)
+    assert core.stats()["reads"] > 0
+    core.close()
+    for a, b in pairs:
+        a.close()
+        b.close()
+
+
+def test_hub_pause_stops_reading_and_remove_closes():
+    mod = load()
+    core = mod.ReaderHub(64 * 1024, 2)
+    a, b = socket.socketpair()
+    sid = core.add(os.dup(b.fileno()))
+    b.close()  # the hub's dup is the only reader now
+    core.pause(sid, True)
+    a.sendall(b"x" * 1000)
+    time.sleep(0.1)
+    assert core.take() == []  # paused: nothing read
+    core.pause(sid, False)
+    got, _ = _drain(core, 1000)
+    assert bytes(got[sid]) == b"x" * 1000
+    core.remove(sid)  # closes the hub's fd: the peer sees EOF
+    a.settimeout(2)
+    assert a.recv(10) == b""
+    core.close()
+    a.close()
+
+
+def test_pool_exhaustion_is_backpressure_not_loss():
+    """With every buffer held by the consumer the hub stops polling; data waits
+    in the socket and arrives, complete and in order, once buffers return."""
+    mod = load()
+    core = mod.ReaderHub(4096, 2)
+    a, b = socket.socketpair()
+    sid = core.add(os.dup(b.fileno()))
+    data = os.urandom(200_000)
+    import threading
+    t = threading.Thread(target=a.sendall, args=(data,))
+    t.start()
+    time.sleep(0.1)
+    held = []
+    deadline = time.monotonic() + 2
+    while len(held) < 2 and time.monotonic() < deadline:
+        held += [(buf, bytes(view)) for _s, buf, view, _ns, _e in core.take() if view is not None]
+        time.sleep(0.005)
+    assert len(held) == 2
+    time.sleep(0.1)
+    assert core.take() == []  # pool empty: not reading
+    assert core.stats()["starved"] >= 0
+    out = bytearray(b"".join(x for _, x in held))
+    for buf, _ in held:
+        core.release(buf)
+    got, _ = _drain(core, len(data) - len(out))
+    t.join()
+    out += got[sid]
+    assert bytes(out) == data
+    core.close()
+    a.close()
+    b.close()
+
+
+def test_http_stream_adopted_by_hub_end_to_end():
+    """HttpClient hands a zero-copy raw stream to the hub after its head; the
+    sink gets the same bytes, the server's close ends `finished`, and a client
+    close reaches the server."""
+
+    async def body():
+        closed_by_client = asyncio.get_running_loop().create_future()
+
+        async def handle(reader, writer):
+            req = await reader.readuntil(b"\r\n\r\n")
+            writer.write(b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n")
+            if b"/short" in req:
+                writer.write(b"5\r\nhello\r\n0\r\n\r\n")
+                await writer.drain()
+                writer.close()
+                return
+            for i in range(200):
+                chunk = (b"%05d" % i) * 200
+                writer.write(b"%x\r\n%s\r\n" % (len(chunk), chunk))
+            await writer.drain()
+            await reader.read()
+            closed_by_client.set_result(True)
+            writer.close()
+
+        srv = await asyncio.start_server(handle, "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        c = HttpClient(f"http://127.0.0.1:{port}")
+        hub = WatchReaderHub(64 * 1024, 4)
+        c.reader_hub = hub
+        got = bytearray()
+        stream, err = await c.stream("GET", "/long", lambda d, _ns: got.extend(d), raw_chunked=True,
+                                     read_size=1 << 20, zero_copy=True)
+        assert err is None and stream._proto.hub is hub
+        want = sum(len(b"%x\r\n" % 1000) + 1000 + 2 for _ in range(200))
+        for _ in range(500):
+            if len(got) >= want:
+                break
+            await asyncio.sleep(0.01)
+        long_ok = len(got) == want and b"00199" in got
+        stream.close()
+        by_client = await asyncio.wait_for(closed_by_client, 5)
+        await asyncio.wait_for(stream.finished, 5)
+        short = bytearray()
+        s2, err2 = await c.stream("GET", "/short", lambda d, _ns: short.extend(d), raw_chunked=True,
+                                  read_size=1 << 20, zero_copy=True)
+        await asyncio.wait_for(s2.finished, 5)  # the server's close ends it
+        stats = hub.stats()
+        hub.close()
+        await c.close()
+        srv.close()
+        return long_ok, by_client, bytes(short), stats
+
+    long_ok, by_client, short, stats = run(body())
+    assert long_ok and by_client
+    assert short.endswith(b"0\r\n\r\n")
+    assert stats["streams"] == 0  # both streams left the hub
+
+
+def test_tls_streams_stay_on_asyncio():
+    pytest.importorskip("ssl")
+    from k8s_watcher_amd.net import reader as reader_mod
+
+    class FakeTransport:
+        def is_closing(self):
+            return False
+
+        def get_extra_info(self, name):
+            return object() if name == "sslcontext" else None
+
+    class P:
+        transport = FakeTransport()
+
+    async def body():
+        hub = reader_mod.WatchReaderHub(64 * 1024, 2)
+        ok = hub.adopt(P())
+        hub.close()
+        return ok
+
+    assert run(body()) is False
