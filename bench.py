@@ -517,6 +517,8 @@ async def rank_main(args, d: Dist) -> dict:
             lat_hi = list(metrics.latency.samples or [])
         failed = c["notify_failed"]
         delivered_total = c["notify_delivered"]
+        hub = getattr(svc, "_reader_hub", None)
+        reader = dict(hub.stats(), mode="native") if hub is not None else {"mode": "asyncio"}
         svc.stop()
         await svc.shutdown()
         d.barrier()  # every shard stopped: the sink's counts are final
@@ -537,7 +539,7 @@ async def rank_main(args, d: Dist) -> dict:
                 "cpu_threads": sorted((round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0
                                        if k.startswith("thread_") and k != "thread_loop" and k in cpu1),
                                       reverse=True)[:8],
-                "decode_threads": decode_threads, "scope": scope, "step_phases_ms": step_phases, "probe": probe,
+                "decode_threads": decode_threads, "scope": scope, "step_phases_ms": step_phases, "probe": probe, "reader": reader,
                 "placement": {"watcher": cpu_ranges(watcher_cpus), "fixtures": cpu_ranges(fx_cpus),
                               "threads": svc.thread_placement}}
     finally:
@@ -711,6 +713,7 @@ def main(argv=None) -> int:
         "sink_workers": res["sink_workers"],
         "cpu_util_rank0": res["cpu_util"],
         "step_phases_ms_rank0": res["step_phases_ms"],
+        "watch_reader_rank0": res["reader"],
         **({"loop_probe_rank0": res["probe"]} if res["probe"] else {}),
         "cpu_other_threads_rank0": res["cpu_threads"],
         # the watcher's own efficiency (the rate is bound by the replay fixture's core when it hits 1.0)

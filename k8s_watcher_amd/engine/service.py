@@ -287,6 +287,10 @@ class WatcherService:
                 self._reader_hub = WatchReaderHub(s.watcher.watch_read_bytes or (4 << 20),
                                                   s.watcher.watch_reader_buffers)
                 self.api.http.reader_hub = self._reader_hub
+                hub = self._reader_hub
+                self.metrics.gauges["watch_reader_streams"] = lambda: float(len(hub.protos))
+                self.metrics.gauges["watch_reader_reads"] = lambda: float(hub.stats().get("reads", 0))
+                self.metrics.gauges["watch_reader_wakeups"] = lambda: float(hub.stats().get("signals", 0))
             self._pin_threads()
         if saved_rvs and None not in scopes:
             # pods of namespaces this shard no longer watches would never be reconciled

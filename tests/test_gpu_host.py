@@ -40,6 +40,19 @@ def test_bench_line_is_valid():
         assert key in line
     assert line["value"] > 0 and line["n_gpus"] == 1 and line["steps"] == 2
     assert line["notify_failed"] == 0
+    # the watch bytes came through the native reader thread, not asyncio
+    assert line["watch_reader_rank0"]["mode"] == "native" and line["watch_reader_rank0"]["reads"] > 0
+    assert line["verify"]["exactly_once"]
+
+
+def test_reader_hub_on_host():
+    """The native watch reader's contract (order, EOF, pause, pool backpressure) on the host's CPUs."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import test_reader_hub
+    test_reader_hub.test_hub_reads_streams_in_order_and_signals_eof()
+    test_reader_hub.test_hub_pause_stops_reading_and_remove_closes()
+    test_reader_hub.test_pool_exhaustion_is_backpressure_not_loss()
+    test_reader_hub.test_http_stream_adopted_by_hub_end_to_end()
 
 
 def test_tls_bench_line_is_valid():
