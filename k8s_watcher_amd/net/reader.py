@@ -26,7 +26,7 @@ from ..ops import native
 
 
 class WatchReaderHub:
-    def __init__(self, buf_bytes: int, nbufs: int = 8,
+    def __init__(self, buf_bytes: int, nbufs: int = 64,
                  loop: Optional[asyncio.AbstractEventLoop] = None) -> None:
         self.loop = loop or asyncio.get_running_loop()
         self.core = native.load().ReaderHub(max(64 * 1024, int(buf_bytes)), max(2, int(nbufs)))

@@ -293,7 +293,7 @@ class WatcherSettings:
     payload_extra: int = 0  # watcher.payload_extra_fields as a models.payload.extra_mask
     watch_read_bytes: int = 4 << 20  # bytes per socket read on a plain-TCP watch (asyncio default 256 KiB)
     watch_reader: str = "native"  # native (ReaderHub thread, plain TCP + native engine) | asyncio
-    watch_reader_buffers: int = 8  # ReaderHub pool: buffers of watch_read_bytes each
+    watch_reader_buffers: int = 64  # ReaderHub pool: up to this many buffers of watch_read_bytes (allocated on use)
     thread_pinning: str = "auto"  # auto: loop thread on its own core when the process sits in one L3 | none
     retry: RetryPolicy = field(default_factory=lambda: RetryPolicy(3, 5.0))
     watch_timeout_seconds: int = 300
@@ -458,7 +458,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         payload_extra=_payload_extra(w.get("payload_extra_fields") or []),
         watch_read_bytes=max(0, _as_int(w.get("watch_read_bytes", 4 << 20), "watcher.watch_read_bytes")),
         watch_reader=_choice(w.get("watch_reader", "native"), "watcher.watch_reader", ("native", "asyncio")),
-        watch_reader_buffers=max(2, _as_int(w.get("watch_reader_buffers", 8), "watcher.watch_reader_buffers")),
+        watch_reader_buffers=max(2, _as_int(w.get("watch_reader_buffers", 64), "watcher.watch_reader_buffers")),
         thread_pinning=_choice(w.get("thread_pinning", "auto"), "watcher.thread_pinning", ("auto", "none")),
         retry=_retry(w.get("retry"), "watcher.retry", RetryPolicy(3, 5.0), min_attempts=0),
         watch_timeout_seconds=_as_int(w.get("watch_timeout_seconds", 300), "watcher.watch_timeout_seconds"),

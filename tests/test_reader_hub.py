@@ -201,3 +201,33 @@ def test_tls_streams_stay_on_asyncio():
         return ok
 
     assert run(body()) is False
+
+
+def test_read_ahead_is_capped_per_stream():
+    """However large the pool, one stream gets at most two buffers ahead of
+    the consumer: a slow event loop leaves the backlog in the socket (TCP flow
+    control), not in user memory."""
+    mod = load()
+    core = mod.ReaderHub(4096, 16)
+    a, b = socket.socketpair()
+    sid = core.add(os.dup(b.fileno()))
+    data = os.urandom(400_000)
+    import threading
+    t = threading.Thread(target=a.sendall, args=(data,))
+    t.start()
+    time.sleep(0.2)
+    held = []
+    for _ in range(20):
+        held += [(buf, bytes(view)) for _s, buf, view, _ns, _e in core.take() if view is not None]
+        time.sleep(0.01)
+    assert 1 <= len(held) <= 2
+    out = bytearray(b"".join(x for _, x in held))
+    for buf, _ in held:
+        core.release(buf)
+    got, _ = _drain(core, len(data) - len(out))
+    t.join()
+    out += got[sid]
+    assert bytes(out) == data
+    core.close()
+    a.close()
+    b.close()
