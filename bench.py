@@ -92,6 +92,9 @@ def parse_args(argv=None):
     ap.add_argument("--thread-pinning", default=None, choices=["auto", "none"], help="watcher.thread_pinning")
     ap.add_argument("--no-placement", dest="placement", action="store_false",
                     help="no per-rank L3 domain assignment (each watcher still pins per watcher.decode_affinity)")
+    ap.add_argument("--front-ends", default="per-rank", choices=["per-rank", "shared"],
+                    help="per-rank: one API-server and one clusterapi front-end per rank, on its L3 domain "
+                         "(one cluster behind them); shared: one of each for every rank, on rank 0's domain")
     ap.add_argument("--fixture-placement", default="inherit", choices=["apart", "inherit"],
                     help="inherit: the API-server fixture and the sink share rank 0's L3 domain, so the watch "
                          "bytes reach the watcher through that cache (as a NIC's DMA into the LLC would); apart: "
@@ -247,44 +250,63 @@ def target_namespaces(spec: str, names):
 
 
 class Fixtures:
-    """Rank 0's cluster fixture + stub clusterapi (shared by every rank)."""
+    """Rank 0's cluster fixture + stub clusterapi, shared by every rank.
+
+    One cluster (one event history, one resourceVersion sequence) behind one
+    API-server front-end per rank — like the replicas of an HA API server —
+    and one stub-clusterapi front-end per rank, all recording into one verify
+    directory. Each front-end runs on its rank's L3 domain (beside the
+    watcher, off its event-loop core), so every rank reads its watch bytes
+    from its own cache the way rank 0 does; with one shared front-end the
+    other ranks' bytes would all cross dies (measured 35-40% slower,
+    profiles/fixture_placement_gpu_box.md)."""
 
     def __init__(self) -> None:
         self.replay = None
-        self.sink = None
+        self.sinks: list = []
         self.info: dict = {}
         self.verify_dir = None
         self.pki = None
 
-    async def start(self, args, world: int, names, targets, cpus=None) -> dict:
-        fw = args.fixture_workers or max(2, 2 * world)
-        self.cpus = cpus
+    async def start(self, args, world: int, names, targets, rank_cpus) -> dict:
+        fronts = world if args.front_ends == "per-rank" else 1
+        rank_cpus = list(rank_cpus) + [None] * (world - len(rank_cpus))
+        fw = args.fixture_workers or (2 if fronts > 1 else max(2, 2 * world))
+        cpu_arg = ";".join(cpu_ranges(rank_cpus[g]) or "" for g in range(fronts)) if any(rank_cpus) else None
         self.replay = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.cluster_replay",
                                   "--pods", str(args.pods_per_step * world),
                                   "--namespace-list", ",".join(names), "--targets", ",".join(targets),
-                                  "--workers", str(fw), cpus=cpus)
-        sink_port = free_port()
+                                  "--workers", str(fw), "--groups", str(fronts),
+                                  *(["--group-cpus", cpu_arg] if cpu_arg else []), cpus=rank_cpus[0])
         tls_args = []
         if args.tls:
             from k8s_watcher_amd.testing.certs import make_pki
             self.pki = make_pki(tempfile.mkdtemp(prefix="bench-pki-"))
             tls_args = ["--tls-cert", self.pki.server_crt, "--tls-key", self.pki.server_key]
-        self.sink_workers = args.sink_workers or 4 * world
+        per_sink = args.sink_workers or (4 if fronts > 1 else 4 * world)
+        self.sink_workers = per_sink * fronts
         verify = []
         if args.verify:
             self.verify_dir = tempfile.mkdtemp(prefix="bench-verify-")
             verify = ["--verify-dir", self.verify_dir]
-        self.sink = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.stub_sink", "--port", str(sink_port),
-                                "--workers", str(self.sink_workers), *tls_args, *verify, cpus=cpus)
+        sink_ports = []
+        for g in range(fronts):
+            sink_ports.append(free_port())
+            self.sinks.append(await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.stub_sink",
+                                          "--port", str(sink_ports[-1]), "--workers", str(per_sink),
+                                          *tls_args, *verify, cpus=rank_cpus[g]))
         line = (await asyncio.wait_for(self.replay.stdout.readline(), 600)).decode()
         assert line.startswith("READY "), line
         self.info = json.loads(line[6:])
-        await asyncio.wait_for(self.sink.stdout.readline(), 60)
+        for sink in self.sinks:
+            await asyncio.wait_for(sink.stdout.readline(), 60)
         await asyncio.sleep(0.3)  # let every SO_REUSEPORT worker bind
         scheme = "https" if args.tls else "http"
-        return {"api_port": self.info["port"], "sink_url": f"{scheme}://127.0.0.1:{sink_port}",
+        ports = self.info.get("ports") or [self.info["port"]]
+        return {"api_ports": [ports[r % len(ports)] for r in range(world)],
+                "sink_urls": [f"{scheme}://127.0.0.1:{sink_ports[r % fronts]}" for r in range(world)],
                 "ns_events": self.info["namespaces"], "events_per_step": self.info["events_per_step"],
-                "notifiable_per_step": self.info["notifiable_per_step"],
+                "notifiable_per_step": self.info["notifiable_per_step"], "front_ends": fronts,
                 "ca": self.pki.ca_crt if self.pki else None, "fixture_workers": self.info["workers"]}
 
     async def cmd(self, line: str) -> list:
@@ -296,7 +318,8 @@ class Fixtures:
         """Snapshot of the sink's key counts over all its workers (SIGUSR1)."""
         for f in glob.glob(os.path.join(self.verify_dir, "sink-*.json")):
             os.unlink(f)
-        os.killpg(self.sink.pid, signal.SIGUSR1)
+        for sink in self.sinks:
+            os.killpg(sink.pid, signal.SIGUSR1)
         deadline = time.monotonic() + 60
         files = []
         while time.monotonic() < deadline:
@@ -322,7 +345,7 @@ class Fixtures:
                 await self.replay.stdin.drain()
             except (ConnectionError, RuntimeError):
                 pass
-        for p in (self.replay, self.sink):
+        for p in (self.replay, *self.sinks):
             if p is None:
                 continue
             try:
@@ -361,17 +384,25 @@ async def rank_main(args, d: Dist) -> dict:
     held = [set(x) for x in d.all_gather(sorted(watcher_cpus) if watcher_cpus else []) if x]
     fx_cpus = None
     if args.fixture_placement == "apart":
-        # by default the fixtures inherit rank 0's pinning (its cores and L3)
+        # by default the fixtures run on the watchers' own L3 domains
         fx_cpus = fixture_cpus(all_cpus, held) if held else all_cpus
     elif watcher_cpus and args.thread_pinning != "none":
         # ... minus the physical core watcher.thread_pinning gives the event-loop thread
         from k8s_watcher_amd.utils.cpus import loop_core_split
         split = loop_core_split(watcher_cpus)
         fx_cpus = split[1] if split else None
+    elif watcher_cpus:
+        fx_cpus = set(watcher_cpus)
+    rank_fx = d.all_gather(sorted(fx_cpus) if fx_cpus else None)  # each rank's front-ends run here
+    rank_fx = [set(x) if x else None for x in rank_fx]
+    if args.fixture_placement == "apart":
+        rank_fx = [fx_cpus] * d.world
     fx = Fixtures()
     try:
-        shared = await fx.start(args, d.world, names, targets, fx_cpus) if d.rank == 0 else None
+        shared = await fx.start(args, d.world, names, targets, rank_fx) if d.rank == 0 else None
         shared = d.broadcast(shared)
+        shared["api_port"] = shared["api_ports"][d.rank]
+        shared["sink_url"] = shared["sink_urls"][d.rank]
         log_path = os.path.join("/tmp", f"k8s-watcher-bench-{os.getpid()}.log")
         setup_logging(args.profile, "WARNING" if args.profile == "production" else "INFO", log_file=log_path)
         overrides = {
@@ -534,6 +565,7 @@ async def rank_main(args, d: Dist) -> dict:
                 "lat": lat, "lat_hi": lat_hi, "sat": sat, "failed": failed, "ref": ref, "verify": verify,
                 "delivered_total": delivered_total, "notifiable": notifiable[0],
                 "fixture_workers": shared["fixture_workers"], "sink_workers": getattr(fx, "sink_workers", None),
+                "front_ends": shared["front_ends"],
                 "cpu_util": {k: round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0
                              if not k.startswith("thread_") or k == "thread_loop"},
                 "cpu_threads": sorted((round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0
@@ -594,7 +626,7 @@ def cpu_snapshot(fx: "Fixtures") -> dict:
     out = {"watcher": t.user + t.system}
     if fx.replay is not None:
         out["replay"] = tree(fx.replay)
-        out["sink"] = tree(fx.sink)
+        out["sink"] = sum(tree(sink) for sink in fx.sinks)
     main = threading.get_native_id()
     for th in psutil.Process().threads():  # per thread: the event loop vs the decode workers
         out["thread_loop" if th.id == main else f"thread_{th.id}"] = th.user_time + th.system_time
@@ -710,6 +742,7 @@ def main(argv=None) -> int:
         "verify": verify,
         "per_rank": per_rank,
         "fixture_workers": res["fixture_workers"],
+        "front_ends": res["front_ends"],
         "sink_workers": res["sink_workers"],
         "cpu_util_rank0": res["cpu_util"],
         "step_phases_ms_rank0": res["step_phases_ms"],

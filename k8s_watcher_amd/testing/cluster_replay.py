@@ -13,7 +13,9 @@ cluster:
   order with one global resourceVersion sequence, as etcd would;
 * served by ``--workers`` processes that each ``listen()`` on the same port
   with ``SO_REUSEPORT`` — the kernel spreads the watch connections, so the
-  fixture is not one core feeding N watchers;
+  fixture is not one core feeding N watchers; ``--groups`` front-ends (one
+  port each, like the replicas of an HA API server) serve the same cluster,
+  each optionally pinned near the watcher that uses it (``--group-cpus``);
 * any namespace watch (``/api/v1/namespaces/<ns>/pods``), the cluster-wide
   watch (``/api/v1/pods``), LISTs of both, ``/api/v1/namespaces`` (LIST and a
   quiet WATCH) and ``/version``.
@@ -485,6 +487,17 @@ def _split_items(arr: bytes) -> List[bytes]:
     return out
 
 
+def _cpu_list(text: str) -> set:
+    out = set()
+    for part in text.split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            out.update(range(int(a), int(b) + 1))
+        elif part.strip():
+            out.add(int(part))
+    return out
+
+
 def _reuseport_socket(port: int, listen: bool) -> socket.socket:
     s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
     s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
@@ -501,27 +514,38 @@ def run(args) -> None:
                   else namespace_names(args.namespaces))
     targets = args.targets.split(",") if args.targets else None
     model = ClusterModel(namespaces, args.pods, args.seed, args.prototypes, targets)
-    reserve = _reuseport_socket(args.port, listen=False)  # holds the port; workers listen on it
-    port = reserve.getsockname()[1]
+    # front-ends: like the replicas of an HA API server, each group of workers
+    # listens on its own port and serves the same cluster (every worker holds
+    # the whole history); a client picks one. --group-cpus pins each group.
+    cpus = [_cpu_list(x) for x in args.group_cpus.split(";")] if args.group_cpus else []
+    groups = max(1, args.groups)
+    reserves = [_reuseport_socket(args.port if g == 0 else 0, listen=False) for g in range(groups)]
+    ports = [r.getsockname()[1] for r in reserves]  # held; the workers listen on them
     workers = []  # (pid, ctrl_w, reply_r)
-    for _ in range(max(1, args.workers)):
-        c_r, c_w = os.pipe()
-        r_r, r_w = os.pipe()
-        pid = os.fork()
-        if pid == 0:
-            os.close(c_w)
-            os.close(r_r)
-            reserve.close()
-            try:
-                asyncio.run(Worker(model, _reuseport_socket(port, listen=True)).serve(c_r, r_w))
-            finally:
-                os._exit(0)
-        os.close(c_r)
-        os.close(r_w)
-        workers.append((pid, os.fdopen(c_w, "wb", buffering=0), os.fdopen(r_r, "rb", buffering=0)))
+    for g in range(groups):
+        for _ in range(max(1, args.workers)):
+            c_r, c_w = os.pipe()
+            r_r, r_w = os.pipe()
+            pid = os.fork()
+            if pid == 0:
+                os.close(c_w)
+                os.close(r_r)
+                for r in reserves:
+                    r.close()
+                try:
+                    if g < len(cpus) and cpus[g]:
+                        os.sched_setaffinity(0, cpus[g])
+                    asyncio.run(Worker(model, _reuseport_socket(ports[g], listen=True)).serve(c_r, r_w))
+                finally:
+                    os._exit(0)
+            os.close(c_r)
+            os.close(r_w)
+            workers.append((pid, os.fdopen(c_w, "wb", buffering=0), os.fdopen(r_r, "rb", buffering=0)))
     for _, _, rd in workers:
         assert rd.readline().strip() == b"READY"
-    info = {"port": port, "events_per_step": model.E, "notifiable_per_step": model.notifiable_upto(model.E),
+    port = ports[0]
+    info = {"port": port, "ports": ports, "events_per_step": model.E,
+            "notifiable_per_step": model.notifiable_upto(model.E),
             "namespaces": {ns: model.events_in(ns) for ns in namespaces}, "workers": len(workers)}
     print("READY " + json.dumps(info, separators=(",", ":")), flush=True)
     for line in sys.stdin:
@@ -562,7 +586,9 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--namespaces", type=int, default=64)
     ap.add_argument("--namespace-list", default=None, help="comma-separated names instead of tenant-NNN")
     ap.add_argument("--targets", default=None, help="namespaces the watchers notify for (notifiable counts)")
-    ap.add_argument("--workers", type=int, default=2)
+    ap.add_argument("--workers", type=int, default=2, help="worker processes per front-end")
+    ap.add_argument("--groups", type=int, default=1, help="front-ends (ports) serving the same cluster")
+    ap.add_argument("--group-cpus", default=None, help="';'-separated CPU lists, one per front-end")
     ap.add_argument("--prototypes", type=int, default=256)
     ap.add_argument("--seed", type=int, default=0)
     run(ap.parse_args(argv))

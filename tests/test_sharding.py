@@ -128,6 +128,7 @@ def test_bench_sharded_ranks_exactly_once(ranks):
     assert d["n_gpus"] == ranks and d["config"]["global_batch"] == ranks * 1500
     assert d["value"] > 0 and d["scaling"] == "weak"
     assert "namespace_scope=discover" in d["config"]["parallelism"]
+    assert d["front_ends"] == ranks  # one API-server and one clusterapi front-end per rank, one cluster
     # every shard watched its own namespaces: 16 in total, split evenly, each event counted once
     assert sum(p["scopes"] for p in d["per_rank"]) == 16, d["per_rank"]
     assert {p["scopes"] for p in d["per_rank"]} == {16 // ranks}, d["per_rank"]
