@@ -281,8 +281,10 @@ class WatcherService:
         if self._native_pipeline():
             self._decode_pool = self._make_decode_pool()
             self.pipeline.attach_native(self._decode_pool)
-            if s.watcher.watch_reader == "native" and self.api.http.ssl_context is None:
-                # plain-TCP watches: socket reads on a native thread (net/reader.py)
+            http = self.api.http
+            if s.watcher.watch_reader == "native" and (http.ssl_context is None
+                                                       or getattr(http.ssl_context, "kw_tls", None) is not None):
+                # watch bodies read (and, for https, decrypted) on a native thread (net/reader.py)
                 from ..net.reader import WatchReaderHub
                 self._reader_hub = WatchReaderHub(s.watcher.watch_read_bytes or (4 << 20),
                                                   s.watcher.watch_reader_buffers)

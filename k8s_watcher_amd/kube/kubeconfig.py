@@ -208,6 +208,14 @@ def build_ssl_context(ca_file: Optional[str] = None, ca_data: Optional[bytes] = 
         ctx = ssl.create_default_context()
     if cert_pem and key_pem:
         _load_cert_chain(ctx, cert_pem, key_pem)
+    # the same trust material for the native watch reader (net/reader.py),
+    # which runs its own OpenSSL session on https watches
+    ca_pem = ca_data
+    if ca_file and not insecure:
+        with open(ca_file, "rb") as fh:
+            ca_pem = (fh.read() + b"\n" + ca_data) if ca_data else fh.read()
+    ctx.kw_tls = {"ca_pem": None if insecure else ca_pem, "cert_pem": cert_pem if key_pem else None,
+                  "key_pem": key_pem if cert_pem else None, "verify": not insecure}
     return ctx
 
 

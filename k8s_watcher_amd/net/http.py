@@ -17,6 +17,7 @@ timeouts and streaming responses.
 from __future__ import annotations
 
 import asyncio
+import socket
 import ssl as _ssl
 import time
 import zlib
@@ -405,9 +406,12 @@ class _ClientProtocol(asyncio.BufferedProtocol):
             self.close()
 
     def hub_eof(self, err: int) -> None:
-        """The hub saw the peer close (err 0) or the socket fail: end the
-        connection through the transport, as a read of EOF would."""
+        """The hub saw the peer close (err 0) or the socket / TLS session fail:
+        end the connection through the transport, as a read of EOF would."""
+        why = self.hub.error_text(self.hub_sid) if err and self.hub is not None else ""
         self._unhub()
+        if why:
+            self._fail(HttpError(why))
         if self.transport is not None:
             self.transport.close()
 
@@ -560,6 +564,33 @@ class HttpClient:
         proto.closed.add_done_callback(lambda _f, p=proto: self._forget(p))
         return proto
 
+    async def _connect_for_hub(self, timeout: float):
+        """A connected plain socket and a protocol whose transport is a
+        :class:`~.reader.HubTransport`, for :meth:`WatchReaderHub.open_tls`."""
+        from .reader import HubTransport
+        loop = asyncio.get_running_loop()
+        sock = None
+        try:
+            infos = await with_timeout(loop.getaddrinfo(self.host, self.port, type=socket.SOCK_STREAM), timeout)
+            family, stype, proto_num, _, addr = infos[0]
+            sock = socket.socket(family, stype, proto_num)
+            sock.setblocking(False)
+            await with_timeout(loop.sock_connect(sock, addr), timeout)
+        except asyncio.TimeoutError:
+            if sock is not None:
+                sock.close()
+            raise HttpError(f"connect to {self.host}:{self.port} timed out") from None
+        except OSError as exc:
+            if sock is not None:
+                sock.close()
+            raise HttpError(f"connect to {self.host}:{self.port} failed: {exc}") from None
+        tune_socket(sock, self.keepalive)
+        proto = _ClientProtocol(loop)
+        proto.connection_made(HubTransport(loop, proto, self.ssl_context))
+        self._all.append(proto)
+        proto.closed.add_done_callback(lambda _f, p=proto: self._forget(p))
+        return proto, sock
+
     async def _acquire(self, timeout: float) -> _ClientProtocol:
         while self._idle:
             proto = self._idle.pop()
@@ -653,8 +684,17 @@ class HttpClient:
         tmo = self.timeout if timeout is None else timeout
         target = self.url_target(path, query)
         raw = build_request(method, target, self.host_header, self._merged_headers(headers), None)
-        proto = await self._connect(tmo)
-        if read_size > 0:
+        hub = self.reader_hub
+        material = getattr(self.ssl_context, "kw_tls", None) if self.ssl_context is not None else None
+        hub_tls = hub is not None and zero_copy and raw_chunked and material is not None
+        sock = None
+        if hub_tls:
+            # https watch: the reader hub owns the connection from the start
+            # (handshake, request, decryption on its thread; net/reader.py)
+            proto, sock = await self._connect_for_hub(tmo)
+        else:
+            proto = await self._connect(tmo)
+        if read_size > 0 and not hub_tls:
             proto.read_size = read_size  # plain TCP: recv_into this many bytes per readiness event
             if hasattr(proto.transport, "max_size"):
                 proto.transport.max_size = read_size
@@ -686,7 +726,15 @@ class HttpClient:
         parser.on_complete = _on_complete
         proto.stream_sink = sink
         assert proto.transport is not None
-        proto.transport.write(raw)
+        if hub_tls:
+            try:
+                hub.open_tls(proto, sock, material, self.server_name, raw)
+            except OSError as exc:
+                proto.close()
+                self._forget(proto)
+                raise HttpError(f"TLS setup for {self.host}:{self.port} failed: {exc}") from None
+        else:
+            proto.transport.write(raw)
         try:
             good = await with_timeout(head_fut, tmo)
         except asyncio.TimeoutError:
@@ -702,9 +750,8 @@ class HttpClient:
             proto.close()
             self._forget(proto)
             return sr, b"".join(err_parts)
-        hub = self.reader_hub
-        if (hub is not None and zero_copy and parser.state == ResponseParser.RAW and self.ssl_context is None
-                and not proto.closed.done()):
+        if (hub is not None and not hub_tls and zero_copy and parser.state == ResponseParser.RAW
+                and self.ssl_context is None and not proto.closed.done()):
             hub.adopt(proto)
         return sr, None
 

@@ -14,6 +14,13 @@ not keep the view).
 The asyncio transport stays the owner of the connection: closing the stream,
 a lost connection and the server's end of the body all go through it, so
 ``StreamResponse.finished`` / ``close()`` behave as before.
+
+An https watch cannot be adopted mid-stream (its TLS session lives in
+Python's ``ssl`` object), so :meth:`open_tls` gives the hub the connection
+from the start: a connected socket, a ``_kwcore.TlsContext`` built from the
+kubeconfig's trust material (``ssl.SSLContext.kw_tls``), the SNI / verified
+host name and the request; the hub runs the handshake and decrypts on its
+thread. A :class:`HubTransport` stands in for the asyncio transport.
 """
 
 from __future__ import annotations
@@ -31,6 +38,7 @@ class WatchReaderHub:
         self.loop = loop or asyncio.get_running_loop()
         self.core = native.load().ReaderHub(max(64 * 1024, int(buf_bytes)), max(2, int(nbufs)))
         self.protos: Dict[int, object] = {}
+        self._tls: Dict[tuple, object] = {}
         self._fd = self.core.fileno()
         self.loop.add_reader(self._fd, self._on_ready)
         self.closed = False
@@ -51,6 +59,27 @@ class WatchReaderHub:
         self.protos[sid] = proto
         proto.hub, proto.hub_sid = self, sid
         return True
+
+    def tls_context(self, material: dict):
+        """``_kwcore.TlsContext`` for an ``ssl.SSLContext``'s ``kw_tls`` material (cached)."""
+        key = (material.get("ca_pem"), material.get("cert_pem"), material.get("key_pem"), material.get("verify"))
+        ctx = self._tls.get(key)
+        if ctx is None:
+            ctx = self._tls[key] = native.load().TlsContext(
+                ca_pem=material.get("ca_pem"), cert_pem=material.get("cert_pem"),
+                key_pem=material.get("key_pem"), verify=bool(material.get("verify", True)))
+        return ctx
+
+    def open_tls(self, proto, sock, material: dict, host: str, request: bytes) -> None:
+        """A connected TCP socket for an https watch: the hub owns it from here
+        on — TLS handshake, the request, then decrypted bytes to ``proto``."""
+        ctx = self.tls_context(material)
+        sid = self.core.add_tls(sock.detach(), ctx, host, request)
+        self.protos[sid] = proto
+        proto.hub, proto.hub_sid = self, sid
+
+    def error_text(self, sid: int) -> str:
+        return "" if self.closed else self.core.error_text(sid)
 
     def forget(self, sid: int) -> None:
         if self.protos.pop(sid, None) is not None and not self.closed:
@@ -95,3 +124,39 @@ class WatchReaderHub:
             proto.close()
         self.protos.clear()
         self.core.close()
+
+
+class HubTransport(asyncio.BaseTransport):
+    """Transport stand-in for a connection the hub owns from the start (TLS):
+    ``close()`` ends it like an asyncio transport would (``connection_lost``
+    on the next loop iteration); reading is flow-controlled through the hub."""
+
+    def __init__(self, loop: asyncio.AbstractEventLoop, proto, sslcontext) -> None:
+        super().__init__()
+        self._loop = loop
+        self._proto = proto
+        self._closing = False
+        self._ssl = sslcontext
+
+    def is_closing(self) -> bool:
+        return self._closing
+
+    def close(self) -> None:
+        if self._closing:
+            return
+        self._closing = True
+        self._loop.call_soon(self._proto.connection_lost, None)
+
+    def get_extra_info(self, name, default=None):
+        if name == "sslcontext":
+            return self._ssl
+        return default
+
+    def write(self, data) -> None:  # the request went to the hub with the socket
+        raise RuntimeError("HubTransport: the request is written by the reader hub")
+
+    def pause_reading(self) -> None:
+        self._proto.set_reading(False)
+
+    def resume_reading(self) -> None:
+        self._proto.set_reading(True)

@@ -170,6 +170,8 @@ def test_decode_pool_lifecycle():
     process may exit while we count."""
     import subprocess
     import sys
+    if "libtsan" in os.environ.get("LD_PRELOAD", ""):
+        pytest.skip("ThreadSanitizer starts a background thread of its own: exact counts do not hold")
     code = ("import os, sys; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
             "from k8s_watcher_amd.ops.native import load\n"
             "from test_native_pipeline import stream\n"
