@@ -105,6 +105,9 @@ def parse_args(argv=None):
                     help="serve the C++ notifier core's sockets on its own thread (clusterapi.pool.io_thread)")
     ap.add_argument("--tls", action="store_true",
                     help="https clusterapi (as production.yaml): the stub sink serves TLS with a throw-away CA")
+    ap.add_argument("--api-tls", action="store_true",
+                    help="https API server (as every real cluster): the replay fixture serves TLS, the watcher "
+                         "verifies it against a throw-away CA")
     ap.add_argument("--sink-workers", type=int, default=None, help="default 4 per rank")
     ap.add_argument("--fixture-workers", type=int, default=None, help="default 2 per rank")
     ap.add_argument("--no-verify", dest="verify", action="store_false",
@@ -273,16 +276,16 @@ class Fixtures:
         rank_cpus = list(rank_cpus) + [None] * (world - len(rank_cpus))
         fw = args.fixture_workers or (2 if fronts > 1 else max(2, 2 * world))
         cpu_arg = ";".join(cpu_ranges(rank_cpus[g]) or "" for g in range(fronts)) if any(rank_cpus) else None
+        if args.tls or args.api_tls:
+            from k8s_watcher_amd.testing.certs import make_pki
+            self.pki = make_pki(tempfile.mkdtemp(prefix="bench-pki-"))
+        api_tls = ["--tls-cert", self.pki.server_crt, "--tls-key", self.pki.server_key] if args.api_tls else []
         self.replay = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.cluster_replay",
                                   "--pods", str(args.pods_per_step * world),
                                   "--namespace-list", ",".join(names), "--targets", ",".join(targets),
-                                  "--workers", str(fw), "--groups", str(fronts),
+                                  "--workers", str(fw), "--groups", str(fronts), *api_tls,
                                   *(["--group-cpus", cpu_arg] if cpu_arg else []), cpus=rank_cpus[0])
-        tls_args = []
-        if args.tls:
-            from k8s_watcher_amd.testing.certs import make_pki
-            self.pki = make_pki(tempfile.mkdtemp(prefix="bench-pki-"))
-            tls_args = ["--tls-cert", self.pki.server_crt, "--tls-key", self.pki.server_key]
+        tls_args = ["--tls-cert", self.pki.server_crt, "--tls-key", self.pki.server_key] if args.tls else []
         per_sink = args.sink_workers or (4 if fronts > 1 else 4 * world)
         self.sink_workers = per_sink * fronts
         verify = []
@@ -307,7 +310,8 @@ class Fixtures:
                 "sink_urls": [f"{scheme}://127.0.0.1:{sink_ports[r % fronts]}" for r in range(world)],
                 "ns_events": self.info["namespaces"], "events_per_step": self.info["events_per_step"],
                 "notifiable_per_step": self.info["notifiable_per_step"], "front_ends": fronts,
-                "ca": self.pki.ca_crt if self.pki else None, "fixture_workers": self.info["workers"]}
+                "ca": self.pki.ca_crt if self.pki else None, "fixture_workers": self.info["workers"],
+                "sink_ca": self.pki.ca_crt if (self.pki and args.tls) else None}
 
     async def cmd(self, line: str) -> list:
         self.replay.stdin.write((line + "\n").encode())
@@ -407,7 +411,7 @@ async def rank_main(args, d: Dist) -> dict:
         setup_logging(args.profile, "WARNING" if args.profile == "production" else "INFO", log_file=log_path)
         overrides = {
             "clusterapi": {"base_url": shared["sink_url"], "timeout": 30,
-                           **({"ca_file": shared["ca"]} if shared["ca"] else {}),
+                           **({"ca_file": shared["sink_ca"]} if shared["sink_ca"] else {}),
                            "enabled": not os.environ.get("BENCH_NO_NOTIFY")},
             "watcher": {"engine": args.engine, "retry": {"max_attempts": 0, "delay_seconds": 0.05},
                         "namespaces": targets,
@@ -435,8 +439,14 @@ async def rank_main(args, d: Dist) -> dict:
         if settings.watcher.log_level:
             setup_logging(args.profile, settings.watcher.log_level, log_file=log_path)
         metrics = Metrics(record_samples=True)
-        svc = WatcherService(settings, endpoint=KubeEndpoint(server=f"http://127.0.0.1:{shared['api_port']}"),
-                             metrics=metrics)
+        if args.api_tls:
+            from k8s_watcher_amd.kube.kubeconfig import build_ssl_context
+            endpoint = KubeEndpoint(server=f"https://127.0.0.1:{shared['api_port']}",
+                                    ssl_context=build_ssl_context(ca_file=shared["ca"]),
+                                    tls_server_name="localhost")
+        else:
+            endpoint = KubeEndpoint(server=f"http://127.0.0.1:{shared['api_port']}")
+        svc = WatcherService(settings, endpoint=endpoint, metrics=metrics)
         await svc.start()
         mine = sorted(r.namespace for r in svc.reflectors if r.namespace) if scope == "discover" else ["*"]
         per_step = (shared["events_per_step"] if mine == ["*"]
@@ -639,7 +649,7 @@ async def run_reference(args, fx: "Fixtures", shared: dict, targets, step: int) 
 
     s = load_settings(args.profile)
     ref = RefEquivWatcher(args.profile, targets, s.watcher.critical_events_only,
-                          shared["sink_url"], ca_file=shared["ca"])
+                          shared["sink_url"], ca_file=shared["sink_ca"])
     loop = asyncio.get_running_loop()
     connected = loop.create_future()
     result = {}
@@ -727,6 +737,7 @@ def main(argv=None) -> int:
             "engine": args.engine,
             "decode_threads": res["decode_threads"],
             "clusterapi": "https" if args.tls else "http",
+            "api_server": "https" if args.api_tls else "http",
             "namespaces": args.namespaces,
             "target_namespaces": len(target_namespaces(args.targets, range(args.namespaces))),
         },

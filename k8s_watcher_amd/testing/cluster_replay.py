@@ -435,9 +435,9 @@ class Worker:
             except ConnectionError:
                 pass
 
-    async def serve(self, ctrl_in: int, ctrl_out: int) -> None:
+    async def serve(self, ctrl_in: int, ctrl_out: int, ssl_ctx=None) -> None:
         loop = asyncio.get_running_loop()
-        server = await asyncio.start_server(self.handle, sock=self.sock, limit=1 << 20)
+        server = await asyncio.start_server(self.handle, sock=self.sock, limit=1 << 20, ssl=ssl_ctx)
         reader = asyncio.StreamReader()
         await loop.connect_read_pipe(lambda: asyncio.StreamReaderProtocol(reader), os.fdopen(ctrl_in, "rb"))
         out = os.fdopen(ctrl_out, "wb", buffering=0)
@@ -535,7 +535,12 @@ def run(args) -> None:
                 try:
                     if g < len(cpus) and cpus[g]:
                         os.sched_setaffinity(0, cpus[g])
-                    asyncio.run(Worker(model, _reuseport_socket(ports[g], listen=True)).serve(c_r, r_w))
+                    ssl_ctx = None
+                    if args.tls_cert:  # https API server (the watcher's TLS path)
+                        import ssl
+                        ssl_ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+                        ssl_ctx.load_cert_chain(args.tls_cert, args.tls_key)
+                    asyncio.run(Worker(model, _reuseport_socket(ports[g], listen=True)).serve(c_r, r_w, ssl_ctx))
                 finally:
                     os._exit(0)
             os.close(c_r)
@@ -588,6 +593,8 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--targets", default=None, help="namespaces the watchers notify for (notifiable counts)")
     ap.add_argument("--workers", type=int, default=2, help="worker processes per front-end")
     ap.add_argument("--groups", type=int, default=1, help="front-ends (ports) serving the same cluster")
+    ap.add_argument("--tls-cert", default=None, help="serve https with this certificate (and --tls-key)")
+    ap.add_argument("--tls-key", default=None)
     ap.add_argument("--group-cpus", default=None, help="';'-separated CPU lists, one per front-end")
     ap.add_argument("--prototypes", type=int, default=256)
     ap.add_argument("--seed", type=int, default=0)

@@ -45,6 +45,18 @@ def test_bench_line_is_valid():
     assert line["verify"]["exactly_once"]
 
 
+def test_https_api_server_bench_line_is_valid():
+    """An https API server (every real cluster) through the hub's native TLS on the host."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                          "--pods-per-step", "1000", "--ref-events", "0", "--latency-seconds", "1",
+                          "--latency-rate-high", "0", "--api-tls"],
+                         capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["config"]["api_server"] == "https" and line["verify"]["exactly_once"]
+    assert line["watch_reader_rank0"]["mode"] == "native"
+
+
 def test_reader_hub_on_host():
     """The native watch reader's contract (order, EOF, pause, pool backpressure) on the host's CPUs."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -53,6 +65,7 @@ def test_reader_hub_on_host():
     test_reader_hub.test_hub_pause_stops_reading_and_remove_closes()
     test_reader_hub.test_pool_exhaustion_is_backpressure_not_loss()
     test_reader_hub.test_http_stream_adopted_by_hub_end_to_end()
+    test_reader_hub.test_read_ahead_is_capped_per_stream()
 
 
 def test_tls_bench_line_is_valid():

@@ -151,6 +151,20 @@ def test_bench_single_rank_cluster_watch():
     assert d["reference_equiv"]["events"] == 200 and d["vs_baseline"] > 0
 
 
+def test_bench_https_api_server_through_the_native_reader():
+    """bench.py --api-tls: the replay API server speaks TLS (as every real
+    cluster does) and the watcher's hub runs the session natively."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--pods-per-step", "300", "--namespaces", "8", "--ref-events", "0", "--api-tls",
+                        "--latency-seconds", "0.5", "--latency-seconds-high", "0.5", "--sink-workers", "1", "--no-placement"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["config"]["api_server"] == "https" and d["verify"]["exactly_once"]
+    assert d["watch_reader_rank0"]["mode"] == "native" and d["watch_reader_rank0"]["reads"] > 0
+    assert d["per_rank"][0]["events"] == 2 * 1500
+
+
 def test_balanced_assignment_bounded_and_stable():
     from k8s_watcher_amd.parallel.shard import balanced_assignment
     names = [f"tenant-{i:03d}" for i in range(67)]
