@@ -434,9 +434,12 @@ class WatcherService:
         return load().DecodePool(n) if n > 0 else 0
 
     def _pin_threads(self) -> None:
-        """``watcher.thread_pinning: auto``: the event-loop thread (which applies
-        every event in stream order, the rate's bound) on a physical core of its
-        own; decode workers and the reader thread on the rest of the L3 domain."""
+        """``watcher.thread_pinning: auto``: keep one physical core of the L3
+        domain free for the event-loop thread (which applies every event in
+        stream order, the rate's bound): the decode workers and the reader
+        thread are pinned to the rest. The loop thread itself stays free to
+        move — pinned hard, it could not escape another process scheduled on
+        its core, and the latency tail grew to ~10 ms (profiles/latency_curve_*)."""
         if self.settings.watcher.thread_pinning != "auto":
             return
         from ..utils.cpus import loop_core_split
@@ -454,13 +457,16 @@ class WatcherService:
             for tid in tids:
                 if tid:
                     os.sched_setaffinity(tid, rest)
-            self._loop_affinity = os.sched_getaffinity(0)  # restored at shutdown
-            os.sched_setaffinity(0, loop_cpus)  # this (the loop) thread; threads it starts later inherit it
+            # the loop thread moves to the free core now (its caches follow
+            # it) but keeps the whole domain to run on
+            self._loop_affinity = os.sched_getaffinity(0)
+            os.sched_setaffinity(0, loop_cpus)
+            os.sched_setaffinity(0, self._loop_affinity)
         except OSError as exc:
             self.log.warning(f"Thread pinning skipped: {exc}")
             return
         self.thread_placement = {"loop": sorted(loop_cpus), "workers": sorted(rest)}
-        self.log.info(f"Event-loop thread pinned to CPUs {sorted(loop_cpus)}; {len(tids)} worker threads to the rest")
+        self.log.info(f"CPUs {sorted(loop_cpus)} kept for the event-loop thread; {len(tids)} worker threads on the rest")
 
     def _native_pipeline(self) -> bool:
         w = self.settings.watcher
