@@ -6,8 +6,8 @@
 | # | BASELINE.json config | how it is run here |
 |---|---|---|
 | 1 | mocked API, 10 pod ADDED events, stub sink | development profile; 10 pods served by the initial LIST |
-| 2 | development.yaml, 100-pod create/delete churn | `createdelete` template: 100 pods × ADDED/MODIFIED/DELETED per round, rounds streamed back to back (sustained rate), DEBUG logging |
-| 3 | staging.yaml, single namespace, 1k pods steady, 10 ev/s MODIFIED | `steady` template: 1000 listed pods; throughput = unthrottled MODIFIED rounds streamed back to back, latency at 10 ev/s |
+| 2 | development.yaml, 100-pod create/delete churn | `createdelete` template: 100 pods × ADDED/MODIFIED/DELETED per round, 1,000 rounds streamed back to back (sustained rate), DEBUG logging |
+| 3 | staging.yaml, single namespace, 1k pods steady, 10 ev/s MODIFIED | `steady` template: 1000 listed pods; throughput = 300 unthrottled MODIFIED rounds streamed back to back, latency at 10 ev/s |
 | 4 | production.yaml, all namespaces, 10k-pod churn, 100 ev/s | `churn` template, 10k lifecycles per step; latency at 100 ev/s (same as bench.py) |
 | 5 | soak: RV bookmark/resume across API-server restarts, 1M events | 20 × 50k churn events with connection drops mid-step (resume), bookmarks and 410 compactions; the sink checks exactly-once |
 
@@ -269,7 +269,7 @@ async def config1(a) -> dict:
 
 
 async def config2(a) -> dict:
-    steps = max(2, int(100 * a.scale))  # 300 events per step: many steps for a stable rate
+    steps = max(2, int(1000 * a.scale))  # 300 events per step: 300k events, a stable sustained rate
     async with Servers("createdelete", 100, prerender=steps + 1) as srv:
         e = srv.events_per_step
         # one stream of `steps` rounds: the sustained rate, not a stop-and-wait per 300-event round
@@ -281,7 +281,7 @@ async def config2(a) -> dict:
 
 
 async def config3(a) -> dict:
-    steps = max(2, int(50 * a.scale))
+    steps = max(2, int(300 * a.scale))  # 1,000 events per step: 300k events
     ov = {"watcher": {"namespaces": ["default"], "namespace_scope": "server"}}
     async with Servers("steady", 1000, prerender=steps + 1, namespaces="default") as srv:
         ours = await run_ours(srv, "staging", ov, [f"STEPS 1 {steps + 1}"], ["STEP 0"],
