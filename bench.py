@@ -87,6 +87,8 @@ def parse_args(argv=None):
     ap.add_argument("--pipeline-depth", type=int, default=None)
     ap.add_argument("--decode-threads", default=None, help="watcher.decode_threads (int or auto)")
     ap.add_argument("--decode-affinity", default=None, choices=["auto", "none", "l3"])
+    ap.add_argument("--decode-spin-us", type=float, default=None,
+                    help="watcher.decode_spin_us: idle decode workers spin this long before sleeping")
     ap.add_argument("--watch-read-bytes", type=int, default=None, help="watcher.watch_read_bytes")
     ap.add_argument("--watch-reader", default=None, choices=["native", "asyncio"], help="watcher.watch_reader")
     ap.add_argument("--thread-pinning", default=None, choices=["auto", "none"], help="watcher.thread_pinning")
@@ -109,6 +111,8 @@ def parse_args(argv=None):
                     help="https API server (as every real cluster): the replay fixture serves TLS, the watcher "
                          "verifies it against a throw-away CA")
     ap.add_argument("--sink-workers", type=int, default=None, help="default 4 per rank")
+    ap.add_argument("--sink-engine", default="auto", choices=["auto", "native", "python"],
+                    help="stub clusterapi request loop (auto: native _kwcore.SinkServer unless --tls)")
     ap.add_argument("--fixture-workers", type=int, default=None, help="default 2 per rank")
     ap.add_argument("--no-verify", dest="verify", action="store_false",
                     help="sink does not count payload keys (no exactly-once proof)")
@@ -297,7 +301,7 @@ class Fixtures:
             sink_ports.append(free_port())
             self.sinks.append(await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.stub_sink",
                                           "--port", str(sink_ports[-1]), "--workers", str(per_sink),
-                                          *tls_args, *verify, cpus=rank_cpus[g]))
+                                          "--engine", args.sink_engine, *tls_args, *verify, cpus=rank_cpus[g]))
         line = (await asyncio.wait_for(self.replay.stdout.readline(), 600)).decode()
         assert line.startswith("READY "), line
         self.info = json.loads(line[6:])
@@ -418,6 +422,7 @@ async def rank_main(args, d: Dist) -> dict:
                         "namespace_scope": "discover" if scope == "discover" else "client",
                         "shard": {"count": d.world, "index": d.rank, "assignment": args.assignment},
                         **({"decode_threads": args.decode_threads} if args.decode_threads is not None else {}),
+                        **({"decode_spin_us": args.decode_spin_us} if args.decode_spin_us is not None else {}),
                         **({"watch_read_bytes": args.watch_read_bytes} if args.watch_read_bytes else {}),
                         **({"watch_reader": args.watch_reader} if args.watch_reader else {}),
                         **({"thread_pinning": args.thread_pinning} if args.thread_pinning else {}),
@@ -517,6 +522,8 @@ async def rank_main(args, d: Dist) -> dict:
             from k8s_watcher_amd.ops import native as _native
             kw = _native.load()
             kw.probe(True)
+        dpool = svc._decode_pool or None
+        pool0 = dpool.stats() if dpool is not None else None
         cpu0 = cpu_snapshot(fx)
         t0 = time.perf_counter()
         if prof is not None:
@@ -531,6 +538,14 @@ async def rank_main(args, d: Dist) -> dict:
             prof.disable()
             prof.dump_stats(os.environ["BENCH_PROFILE"])
         cpu1 = cpu_snapshot(fx)
+        pool_stats = None
+        if dpool is not None:  # decode workers over the timed steps: useful lines vs idle spin/sleep
+            pool1 = dpool.stats()
+            pool_stats = {"spin_us": dpool.spin_us(),
+                          "workers": [{"lines": b["lines"] - a["lines"],
+                                       "spin_frac": round((b["spin_s"] - a["spin_s"]) / elapsed, 3),
+                                       "sleep_frac": round((b["sleep_s"] - a["sleep_s"]) / elapsed, 3),
+                                       "sleeps": b["sleeps"] - a["sleeps"]} for a, b in zip(pool0, pool1)]}
         probe = kw.probe(False) if kw is not None else None
         if probe:
             probe["loop_cpu_ns"] = int((cpu1["thread_loop"] - cpu0["thread_loop"]) * 1e9)
@@ -581,7 +596,7 @@ async def rank_main(args, d: Dist) -> dict:
                 "cpu_threads": sorted((round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0
                                        if k.startswith("thread_") and k != "thread_loop" and k in cpu1),
                                       reverse=True)[:8],
-                "decode_threads": decode_threads, "scope": scope, "step_phases_ms": step_phases, "probe": probe, "reader": reader,
+                "decode_threads": decode_threads, "decode_pool": pool_stats, "scope": scope, "step_phases_ms": step_phases, "probe": probe, "reader": reader,
                 "placement": {"watcher": cpu_ranges(watcher_cpus), "fixtures": cpu_ranges(fx_cpus),
                               "threads": svc.thread_placement}}
     finally:
@@ -758,6 +773,7 @@ def main(argv=None) -> int:
         "cpu_util_rank0": res["cpu_util"],
         "step_phases_ms_rank0": res["step_phases_ms"],
         "watch_reader_rank0": res["reader"],
+        "decode_pool_rank0": res["decode_pool"],
         **({"loop_probe_rank0": res["probe"]} if res["probe"] else {}),
         "cpu_other_threads_rank0": res["cpu_threads"],
         # the watcher's own efficiency (the rate is bound by the replay fixture's core when it hits 1.0)

@@ -431,7 +431,7 @@ class WatcherService:
                                    index=w.decode_l3_domain)
             if dom:
                 self.log.info(f"Decode pool pinned to L3 domain CPUs {sorted(dom)}")
-        return load().DecodePool(n) if n > 0 else 0
+        return load().DecodePool(n, w.decode_spin_us) if n > 0 else 0
 
     def _pin_threads(self) -> None:
         """``watcher.thread_pinning: auto``: keep one physical core of the L3

@@ -26,6 +26,8 @@
 #include <openssl/x509v3.h>
 
 #include <linux/futex.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
 #include <poll.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
@@ -37,6 +39,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cctype>
 #include <cerrno>
 #include <cmath>
 #include <cstdint>
@@ -1917,6 +1920,7 @@ PyObject* kw_bench_parse(PyObject*, PyObject* args) {
 #include "engine.inc"
 #include "checkpoint.inc"
 #include "readerhub.inc"
+#include "sinkserver.inc"
 
 PyMethodDef module_methods[] = {
     {"bench_parse", (PyCFunction)kw_bench_parse, METH_VARARGS, "bench_parse(data, mode=2, repeat=1)"},
@@ -1957,7 +1961,7 @@ PyMODINIT_FUNC PyInit__kwcore(void) {
     Py_INCREF(&ScannerType);
     PyModule_AddObject(m, "ResponseScanner", (PyObject*)&ScannerType);
     if (register_engine(m) < 0 || register_podcache(m) < 0 || register_pipeline(m) < 0 || register_logsink(m) < 0 ||
-        register_checkpoint(m) < 0 || register_readerhub(m) < 0)
+        register_checkpoint(m) < 0 || register_readerhub(m) < 0 || register_sinkserver(m) < 0)
         return nullptr;
     const char* names[6] = {"ADDED", "MODIFIED", "DELETED", "BOOKMARK", "ERROR", "INVALID"};
     for (int i = 0; i < 6; ++i) {

@@ -164,6 +164,41 @@ def test_decode_pool_matches_serial(threads):
     assert [c[0] for c in ctrl] == ["INVALID", "ERROR"] * 3
 
 
+@pytest.mark.parametrize("spin_us", [0.0, 60.0])
+def test_shared_decode_pool_spin_and_stats(spin_us):
+    """A shared pool (the service's) with and without idle spinning decodes
+    exactly the serial result; its per-worker stats account for the lines the
+    workers took, and a pool that does not spin sleeps between feeds."""
+    from k8s_watcher_amd.ops.native import load
+    import time
+    mod = load()
+    with pytest.raises(ValueError):
+        mod.DecodePool(2, -1.0)
+    pool = mod.DecodePool(3, spin_us=spin_us)
+    assert pool.spin_us() == spin_us
+    data = stream()
+    ref = run_python("production", {}, data)
+    s = load_settings("production", environ={})
+    rec, m = Recorder(), Metrics()
+    p = EventPipeline(s, PyDecoder("production"), rec, m)
+    p.log_events_setting = False
+    p.attach_native(pool)
+    lines = data.split(b"\n")
+    half = len(lines) // 2
+    p.handle_raw(b"\n".join(lines[:half]) + b"\n", 0, framed=False)
+    time.sleep(0.01)  # longer than any spin: the workers go to sleep
+    p.handle_raw(b"\n".join(lines[half:]), 0, framed=False)
+    assert rec.calls == ref[0]
+    st = pool.stats()
+    assert len(st) == 3
+    assert sum(w["lines"] for w in st) <= len(lines)
+    assert all(w["spin_s"] >= 0 and w["sleep_s"] >= 0 for w in st)
+    if spin_us == 0.0:
+        assert all(w["sleeps"] >= 1 for w in st)
+    with pytest.raises(Exception):
+        load_settings("production", overrides={"watcher": {"decode_spin_us": -5}}, environ={})
+
+
 def test_decode_pool_lifecycle():
     """Pools are created and joined with their pipelines (no leaked threads).
     Counted in a child process: threads other tests left behind in this
