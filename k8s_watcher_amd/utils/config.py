@@ -310,7 +310,7 @@ class WatcherSettings:
     decode_threads: int = -1  # native engine: extra watch-decode threads, -1 = auto (utils/cpus.py)
     decode_affinity: str = "auto"  # auto | l3 | none: keep loop thread + decode workers in one L3 domain
     decode_l3_domain: int = -1  # with affinity: index into the host's L3 domains, -1 = the current one
-    decode_spin_us: float = 60.0  # idle decode worker spins this long before it sleeps (0 = sleep at once)
+    decode_spin_us: float = 0.0  # idle decode worker spins this long before it sleeps (0 = sleep at once)
     state_format: str = "structured"  # structured | python_repr
     event_timestamp: str = "local"  # local | utc
     log_events: Optional[bool] = None  # None = follow log level (parity)
@@ -476,7 +476,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         decode_threads=_decode_threads(w.get("decode_threads", "auto")),
         decode_affinity=_choice(w.get("decode_affinity", "auto"), "watcher.decode_affinity", ("auto", "l3", "none")),
         decode_l3_domain=_as_int(w.get("decode_l3_domain", -1), "watcher.decode_l3_domain"),
-        decode_spin_us=_bounded_float(w.get("decode_spin_us", 60), "watcher.decode_spin_us", 0.0, 1e6),
+        decode_spin_us=_bounded_float(w.get("decode_spin_us", 0), "watcher.decode_spin_us", 0.0, 1e6),
         state_format=_choice(w.get("state_format", "structured"), "watcher.state_format", ("structured", "python_repr")),
         event_timestamp=_choice(w.get("event_timestamp", "local"), "watcher.event_timestamp", ("local", "utc")),
         log_events=None if w.get("log_events") is None else _as_bool(w.get("log_events"), "watcher.log_events"),
