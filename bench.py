@@ -91,6 +91,8 @@ def parse_args(argv=None):
                     help="watcher.decode_spin_us: idle decode workers spin this long before sleeping")
     ap.add_argument("--watch-read-bytes", type=int, default=None, help="watcher.watch_read_bytes")
     ap.add_argument("--watch-reader", default=None, choices=["native", "asyncio"], help="watcher.watch_reader")
+    ap.add_argument("--watch-reader-buffers", type=int, default=None, help="watcher.watch_reader_buffers")
+    ap.add_argument("--watch-reader-max-bytes", type=int, default=None, help="watcher.watch_reader_max_bytes")
     ap.add_argument("--thread-pinning", default=None, choices=["auto", "none"], help="watcher.thread_pinning")
     ap.add_argument("--no-placement", dest="placement", action="store_false",
                     help="no per-rank L3 domain assignment (each watcher still pins per watcher.decode_affinity)")
@@ -425,6 +427,9 @@ async def rank_main(args, d: Dist) -> dict:
                         **({"decode_spin_us": args.decode_spin_us} if args.decode_spin_us is not None else {}),
                         **({"watch_read_bytes": args.watch_read_bytes} if args.watch_read_bytes else {}),
                         **({"watch_reader": args.watch_reader} if args.watch_reader else {}),
+                        **({"watch_reader_buffers": args.watch_reader_buffers} if args.watch_reader_buffers else {}),
+                        **({"watch_reader_max_bytes": args.watch_reader_max_bytes}
+                           if args.watch_reader_max_bytes is not None else {}),
                         **({"thread_pinning": args.thread_pinning} if args.thread_pinning else {}),
                         # placement already pinned this thread (the decode workers inherit it)
                         **({"decode_affinity": args.decode_affinity or ("none" if watcher_cpus else "auto")})},

@@ -108,6 +108,7 @@ class WatcherService:
         self.spool_replayer = None
         self.ns_watcher: Optional[NamespaceWatcher] = None
         self._scope_tasks: Dict[str, asyncio.Task] = {}
+        self._retiring: Dict[str, asyncio.TimerHandle] = {}  # deleted namespaces draining their pod watch
         self._failure: Optional[asyncio.Future] = None
         self._saved_rvs: Dict[str, Optional[str]] = {}
         self._multi = False  # several (or dynamic) watch scopes, each with its own pipeline
@@ -287,7 +288,8 @@ class WatcherService:
                 # watch bodies read (and, for https, decrypted) on a native thread (net/reader.py)
                 from ..net.reader import WatchReaderHub
                 self._reader_hub = WatchReaderHub(s.watcher.watch_read_bytes or (4 << 20),
-                                                  s.watcher.watch_reader_buffers)
+                                                  s.watcher.watch_reader_buffers,
+                                                  max_bytes=s.watcher.watch_reader_max_bytes)
                 self.api.http.reader_hub = self._reader_hub
                 hub = self._reader_hub
                 self.metrics.gauges["watch_reader_streams"] = lambda: float(len(hub.protos))
@@ -367,6 +369,9 @@ class WatcherService:
             self._failure.set_exception(exc)
 
     def _stop_scope(self, ns: str) -> None:
+        timer = self._retiring.pop(ns, None)
+        if timer is not None:
+            timer.cancel()
         task = self._scope_tasks.pop(ns, None)
         for r in [r for r in self.reflectors if r.namespace == ns]:
             r.stop()
@@ -394,19 +399,63 @@ class WatcherService:
                 cache.pop(uid, None)
 
     def _on_namespaces(self, names: Set[str]) -> None:
-        """NamespaceWatcher callback: start/stop reflectors to match the owned set."""
+        """NamespaceWatcher callback: start/stop reflectors to match the owned set.
+
+        A namespace handed to another shard stops at once (its pods are that
+        shard's business now). A *deleted* namespace drains first: the namespace
+        watch and the namespace's pod watch are separate streams, read in
+        whatever order their bytes arrive, so its pods' DELETED events may still
+        be on the way when the namespace's own DELETED is seen (kube-apiserver
+        deletes the pods before the namespace, but nothing orders two streams)."""
         if not self._live or self._stop.is_set():
             return
         owned = set(self._owned(names))
         current = set(self._scope_tasks)
+        for ns in sorted(owned & set(self._retiring)):  # deleted and created again: keep watching
+            self._retiring.pop(ns).cancel()
         for ns in sorted(owned - current):
             self.metrics.c["scopes_started"] += 1
             self.log.info(f"Watching namespace {ns} (new or now owned by shard {self.settings.watcher.shard.index})")
             self._start_scope(ns, primed=True)
         for ns in sorted(current - owned):
+            if ns not in names:
+                self._retire_scope(ns)
+                continue
             self.metrics.c["scopes_stopped"] += 1
-            self.log.info(f"Stopped watching namespace {ns} (deleted or owned by another shard)")
+            self.log.info(f"Stopped watching namespace {ns} (owned by another shard)")
             self._stop_scope(ns)
+
+    def _cached_in(self, ns: str) -> int:
+        cache = self.pipeline.cache if self.pipeline is not None else None
+        return 0 if cache is None else sum(1 for _uid, ent in cache.items() if ent[2] == ns)
+
+    def _retire_scope(self, ns: str, waited: float = 0.0) -> None:
+        """Keep a deleted namespace's pod watch until every pod cached there has
+        been seen DELETED, or ``watcher.namespace_drain_seconds`` passed; then
+        notify any pod still cached there as DELETED from its cached state (as a
+        relist that no longer finds it would) and stop the watch."""
+        if self._stop.is_set() or ns not in self._scope_tasks:
+            self._retiring.pop(ns, None)
+            return
+        step = 0.05
+        limit = self.settings.watcher.namespace_drain_seconds
+        if self._cached_in(ns) and waited < limit:
+            self._retiring[ns] = asyncio.get_running_loop().call_later(
+                step, self._retire_scope, ns, waited + step)
+            return
+        self._retiring.pop(ns, None)
+        left = [r for r in self.reflectors if r.namespace == ns]
+        if left and self._cached_in(ns):
+            pipe = left[0].pipeline
+            n = self._cached_in(ns)
+            self.metrics.c["namespace_deleted_synthesized"] += n
+            self.log.warning(f"Namespace {ns} deleted: {n} pod(s) without a DELETED event after "
+                             f"{limit:g}s; notifying them as DELETED from the cache")
+            for ev in pipe.reconcile([], time.monotonic_ns(), scope_ns=ns):
+                left[0]._handle_control(ev)
+        self.metrics.c["scopes_stopped"] += 1
+        self.log.info(f"Stopped watching namespace {ns} (deleted)")
+        self._stop_scope(ns)
 
     def _scope_pipeline(self, decoder) -> EventPipeline:
         assert self.pipeline is not None

@@ -34,9 +34,11 @@ from ..ops import native
 
 class WatchReaderHub:
     def __init__(self, buf_bytes: int, nbufs: int = 64,
-                 loop: Optional[asyncio.AbstractEventLoop] = None) -> None:
+                 loop: Optional[asyncio.AbstractEventLoop] = None, max_bytes: int = 0) -> None:
         self.loop = loop or asyncio.get_running_loop()
-        self.core = native.load().ReaderHub(max(64 * 1024, int(buf_bytes)), max(2, int(nbufs)))
+        # max_bytes: read-ahead over all streams (0: the whole pool)
+        self.core = native.load().ReaderHub(max(64 * 1024, int(buf_bytes)), max(2, int(nbufs)),
+                                            max(0, int(max_bytes)))
         self.protos: Dict[int, object] = {}
         self._tls: Dict[tuple, object] = {}
         self._fd = self.core.fileno()

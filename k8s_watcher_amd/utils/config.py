@@ -290,6 +290,7 @@ class WatcherSettings:
     log_file: Optional[str] = None
     namespaces: List[str] = field(default_factory=list)
     namespace_scope: str = "client"  # client | server | discover
+    namespace_drain_seconds: float = 5.0  # discover: a deleted namespace's pod watch runs until its pods are gone
     label_selector: Optional[str] = None
     field_selector: Optional[str] = None
     critical_events_only: bool = False
@@ -301,6 +302,7 @@ class WatcherSettings:
     watch_read_bytes: int = 4 << 20  # bytes per socket read on a plain-TCP watch (asyncio default 256 KiB)
     watch_reader: str = "native"  # native (ReaderHub thread, plain TCP + native engine) | asyncio
     watch_reader_buffers: int = 64  # ReaderHub pool: up to this many buffers of watch_read_bytes (allocated on use)
+    watch_reader_max_bytes: int = 0  # ReaderHub read-ahead over all streams (0: the whole pool)
     thread_pinning: str = "auto"  # auto: loop thread on its own core when the process sits in one L3 | none
     retry: RetryPolicy = field(default_factory=lambda: RetryPolicy(3, 5.0))
     watch_timeout_seconds: int = 300
@@ -456,6 +458,8 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         namespaces=list(namespaces),
         namespace_scope=_choice(w.get("namespace_scope", "client"), "watcher.namespace_scope",
                                 ("client", "server", "discover")),
+        namespace_drain_seconds=_bounded_float(w.get("namespace_drain_seconds", 5), "watcher.namespace_drain_seconds",
+                                               0.0, 3600.0),
         label_selector=w.get("label_selector") or None,
         field_selector=w.get("field_selector") or None,
         critical_events_only=_as_bool(alerts.get("critical_events_only", False), "watcher.alerts.critical_events_only"),
@@ -467,6 +471,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         watch_read_bytes=max(0, _as_int(w.get("watch_read_bytes", 4 << 20), "watcher.watch_read_bytes")),
         watch_reader=_choice(w.get("watch_reader", "native"), "watcher.watch_reader", ("native", "asyncio")),
         watch_reader_buffers=max(2, _as_int(w.get("watch_reader_buffers", 64), "watcher.watch_reader_buffers")),
+        watch_reader_max_bytes=max(0, _as_int(w.get("watch_reader_max_bytes", 0), "watcher.watch_reader_max_bytes")),
         thread_pinning=_choice(w.get("thread_pinning", "auto"), "watcher.thread_pinning", ("auto", "none")),
         retry=_retry(w.get("retry"), "watcher.retry", RetryPolicy(3, 5.0), min_attempts=0),
         watch_timeout_seconds=_as_int(w.get("watch_timeout_seconds", 300), "watcher.watch_timeout_seconds"),

@@ -19,11 +19,16 @@ w = dp.get("workers") or []
 print(f"{sys.argv[2]:22s} {d['value']:>12,.0f} ev/s  ms/step {d['ms_per_step']:7.2f}  cpu {d['cpu_util_rank0']}  "
       f"spin {[x['spin_frac'] for x in w]} sleep {[x['sleep_frac'] for x in w]} "
       f"exactly_once {(d.get('verify') or {}).get('exactly_once')}", flush=True)
+p = d.get("loop_probe_rank0")
+if p:
+    n = max(1, p.get("lines", 1))
+    print(f"{'':22s} probe ns/line: " + " ".join(f"{k[:-3]} {p[k] / n:.0f}" for k in ("split_ns", "wait_ns", "apply_ns", "run_ns") if k in p)
+          + f" notifier_io {p.get('notifier_io_ns', 0) / n:.0f} loop_cpu {p.get('loop_cpu_ns', 0) / n:.0f} lines/call {n / max(1, p.get('calls', 1)):.0f}", flush=True)
 PY
 }
 common="--ref-events 0 --latency-seconds 2 --latency-seconds-high 2"
 IFS=';' read -ra VS <<< "${VARIANTS:-old=--decode-spin-us 60 --sink-engine python;new=}"
-for rep in ${REPS:-1 2 3}; do
+for rep in ${REPS-1 2 3}; do
   for v in "${VS[@]}"; do
     name=${v%%=*}; args=${v#*=}
     tag=n1_${name}_r$rep
@@ -31,8 +36,8 @@ for rep in ${REPS:-1 2 3}; do
     summ $out/$tag.json $tag
   done
 done
-for rep in ${REPS_N:-1 2}; do
-  for n in ${SHARD_NS:-2 4}; do
+for rep in ${REPS_N-1 2}; do
+  for n in ${SHARD_NS-2 4}; do
     for v in "${VS[@]}"; do
       name=${v%%=*}; args=${v#*=}
       tag=n${n}_${name}_r$rep

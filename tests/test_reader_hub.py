@@ -231,3 +231,41 @@ def test_read_ahead_is_capped_per_stream():
     core.close()
     a.close()
     b.close()
+
+
+def test_read_ahead_is_capped_in_bytes_over_all_streams():
+    """``max_bytes``: many streams together hold at most about that many bytes
+    read but not handed back (what the loop reads next stays in cache); the
+    rest waits in the sockets and arrives, complete and in order per stream."""
+    import threading
+    mod = load()
+    core = mod.ReaderHub(64 * 1024, 64, max_bytes=96 * 1024)
+    assert core.stats()["max_bytes"] == 96 * 1024
+    pairs = [socket.socketpair() for _ in range(8)]
+    sids = [core.add(os.dup(b.fileno())) for _a, b in pairs]
+    payload = {sid: os.urandom(150_000) for sid in sids}
+    ths = [threading.Thread(target=a.sendall, args=(payload[sid],)) for (a, _b), sid in zip(pairs, sids)]
+    for t in ths:
+        t.start()
+    time.sleep(0.2)
+    held = []
+    for _ in range(20):
+        held += [(sid, buf, bytes(view)) for sid, buf, view, _ns, _e in core.take() if view is not None]
+        time.sleep(0.01)
+    # one read may overshoot the budget by at most a buffer
+    assert 0 < sum(len(x) for _s, _b, x in held) <= 96 * 1024 + 64 * 1024
+    assert core.stats()["over_budget"] > 0
+    got = {}
+    for sid, buf, x in held:
+        got.setdefault(sid, bytearray()).extend(x)
+        core.release(buf)
+    more, _ = _drain(core, sum(len(v) for v in payload.values()) - sum(len(x) for _s, _b, x in held))
+    for t in ths:
+        t.join()
+    for sid, v in more.items():
+        got.setdefault(sid, bytearray()).extend(v)
+    assert {sid: bytes(v) for sid, v in got.items()} == payload
+    core.close()
+    for a, b in pairs:
+        a.close()
+        b.close()

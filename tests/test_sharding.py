@@ -1,6 +1,7 @@
 """Multi-process sharding (parallel/shard.py, parallel/launch.py) and the
 multi-rank bench path (gloo, world_size 2)."""
 
+import asyncio
 import collections
 import json
 import os
@@ -13,7 +14,7 @@ import time
 
 import pytest
 
-from conftest import ROOT
+from conftest import ROOT, run
 from k8s_watcher_amd.parallel.shard import ShardFilter, shard_of
 from k8s_watcher_amd.testing.fake_apiserver import FakeApiServer, ServerThread
 from k8s_watcher_amd.testing.podgen import PodFactory
@@ -263,3 +264,61 @@ def test_discover_scope_two_shards_exactly_once(assignment):
         await srv.stop()
 
     run(body(), timeout=60)
+
+
+@pytest.mark.parametrize("pod_events", [True, False])
+def test_deleted_namespace_drains_then_synthesizes_deleted(pod_events):
+    """A deleted namespace's pod watch keeps running until its pods are seen
+    DELETED; pods whose DELETED never comes (lost with the stream) are notified
+    DELETED from the cache after ``watcher.namespace_drain_seconds``."""
+    from k8s_watcher_amd.engine.service import WatcherService
+    from k8s_watcher_amd.kube.kubeconfig import KubeEndpoint
+    from k8s_watcher_amd.metrics import Metrics
+
+    async def body():
+        nss = ["keep", "doomed"]
+        srv = FakeApiServer(namespaces=nss)
+        await srv.start()
+        sink = StubSink()
+        await sink.start()
+        s = load_settings("staging", overrides={
+            "clusterapi": {"base_url": sink.url, "health_check_on_start": False},
+            "watcher": {"namespace_scope": "discover", "namespace_drain_seconds": 0.5,
+                        "retry": {"delay_seconds": 0.05, "max_attempts": 0}}})
+        svc = WatcherService(s, endpoint=KubeEndpoint(server=srv.url), metrics=Metrics())
+        await svc.start()
+        f = PodFactory(seed=9, namespaces=nss)
+        doomed = [srv.create(f.new_pod(namespace="doomed"))["metadata"]["uid"] for _ in range(4)]
+        srv.create(f.new_pod(namespace="keep"))
+        await sink.state.wait_for(5, timeout=10)
+        t0 = time.monotonic()
+        if pod_events:
+            srv.delete_namespace("doomed")
+        else:  # the namespace goes, its pods' DELETED events never reach the watcher
+            for key in [k for k in srv.pods if k[0] == "doomed"]:
+                del srv.pods[key]
+            srv.deleted_namespaces.add("doomed")
+            srv._known_ns.discard("doomed")
+            srv._ns_event("DELETED", "doomed")
+        await sink.state.wait_for(9, timeout=10)
+        for _ in range(100):
+            if not any(r.namespace == "doomed" for r in svc.reflectors):
+                break
+            await asyncio.sleep(0.05)
+        took = time.monotonic() - t0
+        got = collections.Counter((p["uid"], p["event_type"]) for p in sink.state.payloads())
+        synth = svc.metrics.c["namespace_deleted_synthesized"]
+        stopped = not any(r.namespace == "doomed" for r in svc.reflectors)
+        svc.stop()
+        await svc.shutdown()
+        await sink.stop()
+        await srv.stop()
+        return doomed, got, synth, stopped, took
+
+    doomed, got, synth, stopped, took = run(body(), timeout=60)
+    assert stopped
+    assert all(got[(u, "DELETED")] == 1 for u in doomed)
+    if pod_events:
+        assert synth == 0 and took < 0.5 + 1.0  # stopped as soon as the pods were gone
+    else:
+        assert synth == 4 and took >= 0.45
