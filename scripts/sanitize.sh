@@ -20,14 +20,14 @@ LD_PRELOAD="$(g++ -print-file-name=libasan.so):$(g++ -print-file-name=libubsan.s
 ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
   timeout -k 10 900 python -m pytest -q -p no:cacheprovider --timeout 300 \
   tests/test_native_parity.py tests/test_native_pipeline.py tests/test_podcache.py tests/test_notifier.py \
-  tests/test_spool.py tests/test_notifier_tls.py tests/test_watch_list.py tests/test_e2e_slice.py tests/test_reflector.py tests/test_http_metrics.py tests/test_reader_hub.py tests/test_reader_hub_tls.py \
+  tests/test_spool.py tests/test_notifier_tls.py tests/test_watch_list.py tests/test_e2e_slice.py tests/test_reflector.py tests/test_http_metrics.py tests/test_reader_hub.py tests/test_reader_hub_tls.py tests/test_native_sink.py \
   2>&1 | tee build/asan.log | tail -3
 echo "== TSan"
 K8S_WATCHER_KWCORE_SO=build/sanitize-thread/$SO \
 LD_PRELOAD="$(g++ -print-file-name=libtsan.so)" TSAN_OPTIONS=report_signal_unsafe=0:halt_on_error=1 \
   timeout -k 10 900 python -m pytest -q -s -p no:cacheprovider --timeout 300 \
   tests/test_native_pipeline.py tests/test_e2e_slice.py tests/test_reflector.py tests/test_native_parity.py \
-  tests/test_notifier.py tests/test_notifier_tls.py tests/test_spool.py tests/test_leader.py tests/test_reader_hub.py tests/test_reader_hub_tls.py \
+  tests/test_notifier.py tests/test_notifier_tls.py tests/test_spool.py tests/test_leader.py tests/test_reader_hub.py tests/test_reader_hub_tls.py tests/test_native_sink.py tests/test_sharding.py \
   2>&1 | tee build/tsan.log | tail -3
 if grep -q "WARNING: ThreadSanitizer\|ERROR: AddressSanitizer\|runtime error:" build/asan.log build/tsan.log; then
   echo "sanitizer reports found (build/asan.log, build/tsan.log)"; exit 1
