@@ -290,6 +290,7 @@ class Fixtures:
                                   "--pods", str(args.pods_per_step * world),
                                   "--namespace-list", ",".join(names), "--targets", ",".join(targets),
                                   "--workers", str(fw), "--groups", str(fronts), *api_tls,
+                                  "--notify", "critical" if args.profile == "production" else "all",
                                   *(["--group-cpus", cpu_arg] if cpu_arg else []), cpus=rank_cpus[0])
         tls_args = ["--tls-cert", self.pki.server_crt, "--tls-key", self.pki.server_key] if args.tls else []
         per_sink = args.sink_workers or (4 if fronts > 1 else 4 * world)

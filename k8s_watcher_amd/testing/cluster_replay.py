@@ -89,7 +89,7 @@ class ClusterModel:
     """The cluster's per-step event history (built once, before the workers fork)."""
 
     def __init__(self, namespaces: List[str], pods: int, seed: int = 0, prototypes: int = 256,
-                 targets: Optional[List[str]] = None, interleave: int = 64) -> None:
+                 targets: Optional[List[str]] = None, interleave: int = 64, critical_only: bool = True) -> None:
         self.namespaces = list(namespaces)
         self.pods = pods
         f = PodFactory(seed, ["proto-ns"])
@@ -137,7 +137,10 @@ class ClusterModel:
         critical = (self.ev_stage == 4) | phase_terminal[proto, self.ev_stage]
         tset = set(targets if targets is not None else self.namespaces)
         is_target = np.array([ns in tset for ns in self.namespaces])
-        self.notifiable = critical & is_target[self.ev_ns]
+        # what the watchers notify: the production profile's critical-events
+        # filter (critical_only), then the namespace filter; other profiles notify
+        # every event in a target namespace
+        self.notifiable = (critical if critical_only else np.ones(self.E, dtype=bool)) & is_target[self.ev_ns]
         self.ns_index = {ns: i for i, ns in enumerate(self.namespaces)}
 
     def events_in(self, ns: str) -> int:
@@ -513,7 +516,8 @@ def run(args) -> None:
     namespaces = (args.namespace_list.split(",") if args.namespace_list
                   else namespace_names(args.namespaces))
     targets = args.targets.split(",") if args.targets else None
-    model = ClusterModel(namespaces, args.pods, args.seed, args.prototypes, targets)
+    model = ClusterModel(namespaces, args.pods, args.seed, args.prototypes, targets,
+                         critical_only=args.notify == "critical")
     # front-ends: like the replicas of an HA API server, each group of workers
     # listens on its own port and serves the same cluster (every worker holds
     # the whole history); a client picks one. --group-cpus pins each group.
@@ -596,6 +600,9 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--tls-cert", default=None, help="serve https with this certificate (and --tls-key)")
     ap.add_argument("--tls-key", default=None)
     ap.add_argument("--group-cpus", default=None, help="';'-separated CPU lists, one per front-end")
+    ap.add_argument("--notify", default="critical", choices=["critical", "all"],
+                    help="which events of the target namespaces count as notifiable: the production "
+                         "profile's critical-events filter, or every one (development/staging)")
     ap.add_argument("--prototypes", type=int, default=256)
     ap.add_argument("--seed", type=int, default=0)
     run(ap.parse_args(argv))
