@@ -107,6 +107,7 @@ def parse_args(argv=None):
     ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
     ap.add_argument("--io-thread", action="store_true",
                     help="serve the C++ notifier core's sockets on its own thread (clusterapi.pool.io_thread)")
+    ap.add_argument("--io-thread-auto", action="store_true", help="clusterapi.pool.io_thread: auto")
     ap.add_argument("--tls", action="store_true",
                     help="https clusterapi (as production.yaml): the stub sink serves TLS with a throw-away CA")
     ap.add_argument("--api-tls", action="store_true",
@@ -444,6 +445,8 @@ async def rank_main(args, d: Dist) -> dict:
             pool["native"] = False
         if args.io_thread:
             pool["io_thread"] = True
+        elif args.io_thread_auto:
+            pool["io_thread"] = "auto"
         if pool:
             overrides["clusterapi"]["pool"] = pool
         settings = load_settings(args.profile, overrides=overrides)

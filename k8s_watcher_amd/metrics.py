@@ -54,6 +54,7 @@ COUNTERS = (
     "namespace_changes",    # namespace set changes seen by watcher.namespace_scope: discover
     "scopes_started",       # per-namespace pod watches opened after start-up (new or handed-over namespaces)
     "scopes_stopped",       # ... and closed (namespace deleted or now owned by another shard)
+    "notify_io_switches",   # clusterapi.pool.io_thread: auto — sockets handed between loop and I/O thread
     "namespace_deleted_synthesized",  # pods of a deleted namespace notified DELETED from the cache (no event came)
     "leader_acquired",      # leadership terms started (engine/leader.py)
     "leader_lost",

@@ -110,6 +110,14 @@ class NativeNotifierPool:
             self._py_fd = self.core.start_io()
             self.loop.add_reader(self._py_fd, self._on_io_signal)
         self._watchdog = self.loop.create_task(self._watchdog_loop())
+        # io_thread: auto — the loop serves the sockets while notifications are
+        # few (lowest latency: no cross-thread hand-off per request); above
+        # io_thread_on_rate the I/O thread takes them (the loop keeps its time
+        # for decoding and applying events), below io_thread_off_rate they
+        # come back. Sampled every 100 ms; switching needs two samples in a row.
+        self._auto = None
+        if settings.pool.io_thread_auto:
+            self._auto = self.loop.create_task(self._auto_io_loop())
 
     # ------------------------------------------------------------------ spool (parallel/spool.py)
     def attach_spool(self, spool) -> None:
@@ -196,6 +204,8 @@ class NativeNotifierPool:
     async def close(self) -> None:
         self.closing = True
         self._watchdog.cancel()
+        if self._auto is not None:
+            self._auto.cancel()
         if self._throttle_timer is not None:
             self._throttle_timer.cancel()
         for h in self.reconnect.values():
@@ -271,6 +281,52 @@ class NativeNotifierPool:
             self.loop.remove_writer(fd)
             self.writers.discard(i)
         sock.close()
+
+    def set_io_thread(self, on: bool) -> None:
+        """Hand the sockets to the core's I/O thread (``on``) or back to the loop."""
+        if on == self.threaded or self.closing:
+            return
+        if on:
+            for sock in self.socks.values():
+                self.loop.remove_reader(sock.fileno())
+            for i in list(self.writers):
+                sock = self.socks.get(i)
+                if sock is not None:
+                    self.loop.remove_writer(sock.fileno())
+            self.writers.clear()
+            self._py_fd = self.core.start_io()  # registers every attached socket with the thread
+            self.loop.add_reader(self._py_fd, self._on_io_signal)
+            self.threaded = True
+            if self.saturated:  # the thread wakes us once the queue has drained enough
+                self.core.signal_below(self.low_water, self.low_bytes)
+        else:
+            self.loop.remove_reader(self._py_fd)
+            self.core.stop_io()  # joins the thread; sockets stay attached
+            self._py_fd = -1
+            self.threaded = False
+            for i, sock in self.socks.items():
+                self.loop.add_reader(sock.fileno(), self._readable, i)
+        self.metrics.c["notify_io_switches"] += 1
+        self._after()  # writers for unsent bytes, counters
+
+    async def _auto_io_loop(self) -> None:
+        on, off = self.settings.pool.io_thread_on_rate, self.settings.pool.io_thread_off_rate
+        period = 0.1
+        c = self.metrics.c
+        last = c["notify_submitted"]
+        streak = 0
+        while True:
+            await asyncio.sleep(period)
+            if self.threaded:
+                self._after()  # counters the I/O thread has not signalled yet
+            now = c["notify_submitted"]
+            rate = (now - last) / period
+            last = now
+            want = rate >= on if not self.threaded else not (rate < off and self.core.pending() == 0)
+            streak = streak + 1 if want != self.threaded else 0
+            if streak >= 2:
+                streak = 0
+                self.set_io_thread(want)
 
     # ------------------------------------------------------------------ loop callbacks
     def _on_io_signal(self) -> None:

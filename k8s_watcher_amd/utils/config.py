@@ -221,6 +221,9 @@ class NotifierPoolSettings:
     coalesce: bool = False
     native: bool = True  # C++ notifier core (watcher.engine: native)
     io_thread: bool = False  # native core serves its sockets on a dedicated thread (profiles/notifier_io_thread_gpu_box.md)
+    io_thread_auto: bool = False  # io_thread: auto — on while notifications run above io_thread_on_rate
+    io_thread_on_rate: float = 50000.0  # notifications/s (auto): hand the sockets to the I/O thread
+    io_thread_off_rate: float = 5000.0  # notifications/s (auto): back to the event loop (low latency)
 
 
 @dataclass
@@ -512,7 +515,13 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
                                                   "clusterapi.pool.max_queued_bytes")),
             coalesce=_as_bool(pool.get("coalesce", False), "clusterapi.pool.coalesce"),
             native=_as_bool(pool.get("native", True), "clusterapi.pool.native"),
-            io_thread=_as_bool(pool.get("io_thread", False), "clusterapi.pool.io_thread"),
+            io_thread=(pool.get("io_thread") != "auto"
+                       and _as_bool(pool.get("io_thread", False), "clusterapi.pool.io_thread")),
+            io_thread_auto=pool.get("io_thread") == "auto",
+            io_thread_on_rate=_bounded_float(pool.get("io_thread_on_rate", 50000), "clusterapi.pool.io_thread_on_rate",
+                                             1.0, 1e9),
+            io_thread_off_rate=_bounded_float(pool.get("io_thread_off_rate", 5000),
+                                              "clusterapi.pool.io_thread_off_rate", 0.0, 1e9),
         ),
         verify_tls=_as_bool(c.get("verify_tls", True), "clusterapi.verify_tls"),
         ca_file=c.get("ca_file") or None,

@@ -403,3 +403,48 @@ def test_compat_clients_honour_retry_after():
 
     t_async, t_sync = run(body())
     assert t_async >= 0.18 and t_sync >= 0.18
+
+
+def test_io_thread_auto_switches_both_ways_without_loss():
+    """``clusterapi.pool.io_thread: auto``: a burst above ``io_thread_on_rate``
+    hands the sockets to the I/O thread, a quiet spell hands them back; every
+    notification is delivered exactly once across the switches, per pod in order."""
+    import dataclasses
+
+    async def body():
+        sink = StubSink(latency=0.002)  # responses lag: requests are in flight while switching
+        await sink.start()
+        m = Metrics(record_samples=True)
+        s = settings(sink.url, depth=4)
+        s = dataclasses.replace(s, pool=dataclasses.replace(s.pool, io_thread_auto=True, io_thread_on_rate=500.0,
+                                                            io_thread_off_rate=100.0))
+        pool = NativeNotifierPool(s, m)
+        sent = []
+        modes = []
+        for burst in range(3):
+            t_end = time.monotonic() + 0.6
+            k = 0
+            while time.monotonic() < t_end:  # ~2,000/s for 0.6 s
+                uid = f"u{k % 50}"
+                pool.submit(uid, "MODIFIED", "default", f"b{burst}-{k}", core(uid, name=f"b{burst}-{k}"), 0, TS)
+                sent.append((uid, f"b{burst}-{k}"))
+                k += 1
+                pool.flush()
+                await asyncio.sleep(0.0005)
+            modes.append(pool.threaded)
+            assert await pool.drain(10)
+            await asyncio.sleep(0.5)  # quiet: back to the loop
+            modes.append(pool.threaded)
+        got = [(p["uid"], p["name"]) for p in sink.state.payloads()]
+        await close(sink, pool)
+        return sent, got, modes, m
+
+    sent, got, modes, m = run(body(), timeout=60)
+    assert True in modes and modes[-1] is False
+    assert m.c["notify_io_switches"] >= 2
+    assert sorted(got) == sorted(sent) and len(got) == len(set(got))  # exactly once
+    by_uid = {}
+    for uid, name in got:
+        by_uid.setdefault(uid, []).append(name)
+    order = {name: i for i, (_u, name) in enumerate(sent)}
+    assert all(seq == sorted(seq, key=order.get) for seq in by_uid.values())  # per pod in order
