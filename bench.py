@@ -127,6 +127,10 @@ def parse_args(argv=None):
     ap.add_argument("--ref-events", type=int, default=10000,
                     help="events for the reference-equivalent run (0 = skip, vs_baseline null)")
     ap.add_argument("--step-timeout", type=float, default=300.0)
+    ap.add_argument("--step-sync", default="stream", choices=["stream", "barrier"],
+                    help="timed steps: stream = rank 0 queues the K steps back to back at the fixture and each "
+                         "rank waits for its cumulative share (one barrier on each side of the K steps); "
+                         "barrier = every rank meets at a barrier after each step")
     ap.add_argument("--probe", action="store_true",
                     help="time the event-loop thread's native calls (split / decode wait / apply / notifier I/O)")
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
@@ -517,6 +521,46 @@ async def rank_main(args, d: Dist) -> dict:
                 print(f"rank {d.rank} step {k}: {time.perf_counter() - t_start:.3f}s", file=sys.stderr)
             await d.abarrier()
 
+        async def run_stream(k0: int, steps: int, expect: int) -> None:
+            """``steps`` steps back to back: the fixture is handed step k+1 as soon
+            as it has sent step k, so no rank idles between steps waiting for the
+            slowest one; the clock still stops only when every event of every
+            step is in and every notification is acknowledged."""
+            base = target[0]
+            target[0] += expect * steps
+            t_start = time.perf_counter()
+
+            async def send_all() -> int:
+                n = 0
+                for k in range(k0, k0 + steps):
+                    n += int((await fx.cmd(f"STEP {k}"))[3])
+                return n
+
+            sent = asyncio.ensure_future(send_all()) if d.rank == 0 else None
+            deadline = time.monotonic() + args.step_timeout * steps
+            t_first = t_all = t_sent = None
+            while c["events_received"] < target[0] or svc.notifier.outstanding() > 0:
+                if t_first is None and c["events_received"] > base:
+                    t_first = time.perf_counter()
+                if t_all is None and c["events_received"] >= target[0]:
+                    t_all = time.perf_counter()
+                if t_sent is None and sent is not None and sent.done():
+                    t_sent = time.perf_counter()
+                if time.monotonic() > deadline or (sent is not None and sent.done() and sent.exception()):
+                    if sent is not None and sent.done() and sent.exception():
+                        raise sent.exception()
+                    raise TimeoutError(f"rank {d.rank} steps {k0}..{k0 + steps - 1}: {c['events_received'] - base}/"
+                                       f"{expect * steps} events, {svc.notifier.outstanding()} notifications "
+                                       f"outstanding")
+                await asyncio.sleep(0.0005)
+            t_end = time.perf_counter()
+            if sent is not None:
+                notifiable[0] += await sent
+            phases.append({"first_event": (t_first or t_end) - t_start,
+                           "fixture_sent": ((t_sent or t_end) - t_start) / steps,
+                           "all_events": ((t_all or t_end) - t_start) / steps, "drained": (t_end - t_start) / steps})
+            await d.abarrier()
+
         for k in range(args.warmup):
             await run_step(k, per_step)
         metrics.latency.reset()
@@ -538,8 +582,11 @@ async def rank_main(args, d: Dist) -> dict:
         if prof is not None:
             prof.enable()
         phases.clear()
-        for k in range(args.warmup, args.warmup + args.steps):
-            await run_step(k, per_step)
+        if args.step_sync == "stream":
+            await run_stream(args.warmup, args.steps, per_step)
+        else:
+            for k in range(args.warmup, args.warmup + args.steps):
+                await run_step(k, per_step)
         elapsed = time.perf_counter() - t0
         step_phases = {key: round(sum(p[key] for p in phases) / len(phases) * 1000, 2) for key in phases[0]} \
             if phases else None
@@ -781,6 +828,7 @@ def main(argv=None) -> int:
         "sink_workers": res["sink_workers"],
         "cpu_util_rank0": res["cpu_util"],
         "step_phases_ms_rank0": res["step_phases_ms"],
+        "step_sync": args.step_sync,
         "watch_reader_rank0": res["reader"],
         "decode_pool_rank0": res["decode_pool"],
         **({"loop_probe_rank0": res["probe"]} if res["probe"] else {}),
