@@ -427,7 +427,7 @@ class WatcherService:
 
     def _cached_in(self, ns: str) -> int:
         cache = self.pipeline.cache if self.pipeline is not None else None
-        return 0 if cache is None else sum(1 for _uid, ent in cache.items() if ent[2] == ns)
+        return 0 if cache is None else cache.count_namespace(ns)
 
     def _retire_scope(self, ns: str, waited: float = 0.0) -> None:
         """Keep a deleted namespace's pod watch until every pod cached there has

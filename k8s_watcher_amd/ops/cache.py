@@ -74,6 +74,9 @@ class PodCache:
     def items(self) -> List[Tuple[str, list]]:
         return list(self.entries.items())
 
+    def count_namespace(self, ns: Optional[str]) -> int:
+        return sum(1 for ent in self.entries.values() if ent[NS] == ns)
+
     def to_records(self) -> List[list]:
         return [[uid] + ent[:4] + [ent[CORE].decode("utf-8") if ent[CORE] else None]
                 for uid, ent in self.entries.items()]

@@ -61,3 +61,16 @@ def test_native_cache_checkpoint_round_trip(tmp_path):
     assert snapshot(loaded) == snapshot(nat)
     _, py, _, _ = load_checkpoint(path)
     assert snapshot(py) == snapshot(nat)
+
+
+def test_count_namespace_native_matches_python():
+    from k8s_watcher_amd.ops.cache import PodCache
+    from k8s_watcher_amd.ops.native import load
+    caches = [load().PodCache(), PodCache()]
+    for c in caches:
+        for i in range(30):
+            c.put(f"u{i}", str(i), "Running", None if i % 7 == 0 else f"ns{i % 3}", f"p{i}", None)
+        c.pop("u4")
+    for ns in ("ns0", "ns1", "ns2", "nope", None):
+        assert caches[0].count_namespace(ns) == caches[1].count_namespace(ns)
+    assert caches[0].count_namespace("nope") == 0
