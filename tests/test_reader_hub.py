@@ -269,3 +269,65 @@ def test_read_ahead_is_capped_in_bytes_over_all_streams():
     for a, b in pairs:
         a.close()
         b.close()
+
+
+def test_take_and_remove_race_the_reader_thread():
+    """The hub thread recv()s outside its lock. Under a steady flood on many
+    streams, takes that land while it is appending to an entry, releases, and
+    removals of streams it is reading must keep every stream's bytes a gap-free,
+    in-order prefix of what was sent (complete for the streams never removed)."""
+    import random
+    import threading
+    mod = load()
+    core = mod.ReaderHub(64 * 1024, 16)
+    pairs = [socket.socketpair() for _ in range(12)]
+    for a, _b in pairs:
+        a.setblocking(True)
+    sids = [core.add(os.dup(b.fileno())) for _a, b in pairs]
+    payload = {sid: os.urandom(600_000) for sid in sids}
+    stop = threading.Event()
+
+    def send(a, data):
+        try:
+            for i in range(0, len(data), 8192):
+                if stop.is_set():
+                    return
+                a.sendall(data[i:i + 8192])
+        except OSError:  # the hub closed a removed stream
+            pass
+
+    ths = [threading.Thread(target=send, args=(a, payload[sid]), daemon=True) for (a, _b), sid in zip(pairs, sids)]
+    for t in ths:
+        t.start()
+    rng = random.Random(3)
+    to_remove = set(rng.sample(sids, 4))
+    gone = set()
+    got = {sid: bytearray() for sid in sids}
+    deadline = time.monotonic() + 20
+    want = sum(len(payload[s]) for s in sids if s not in to_remove)
+    while time.monotonic() < deadline:
+        for sid, buf, view, _ns, _err in core.take():
+            if view is not None:
+                got[sid].extend(view)
+                view.release()
+                core.release(buf)
+        for sid in sorted(to_remove - gone):
+            if len(got[sid]) > 100_000 and rng.random() < 0.2:
+                core.remove(sid)  # usually while the thread is reading it
+                gone.add(sid)
+        if sum(len(got[s]) for s in sids if s not in to_remove) >= want and gone == to_remove:
+            break
+        time.sleep(0.0002)
+    stop.set()
+    assert gone == to_remove
+    for sid in sids:
+        assert bytes(got[sid]) == payload[sid][:len(got[sid])]  # in order, no gap
+        if sid not in to_remove:
+            assert len(got[sid]) == len(payload[sid])
+    core.close()
+    for _a, b in pairs:  # senders blocked on a removed stream now fail and exit
+        b.close()
+    for t in ths:
+        t.join(10)
+    for a, _b in pairs:
+        a.close()
