@@ -31,6 +31,8 @@ IFS=';' read -ra VS <<< "${VARIANTS:-old=--decode-spin-us 60 --sink-engine pytho
 for rep in ${REPS-1 2 3}; do
   for v in "${VS[@]}"; do
     name=${v%%=*}; args=${v#*=}
+    # "SO:<path> rest": this variant loads another build of the extension ($K8S_WATCHER_KWCORE_SO)
+    if [[ $args == SO:* ]]; then so=${args%% *}; export K8S_WATCHER_KWCORE_SO=${so#SO:}; args=${args#"$so"}; else unset K8S_WATCHER_KWCORE_SO; fi
     tag=n1_${name}_r$rep
     timeout -k 10 240 python bench.py $common $args --json-out $out/$tag.json > $out/$tag.log 2>&1 || { echo "$tag failed"; tail -20 $out/$tag.log; exit 1; }
     summ $out/$tag.json $tag
