@@ -114,7 +114,8 @@ class NativeNotifierPool:
         # few (lowest latency: no cross-thread hand-off per request); above
         # io_thread_on_rate the I/O thread takes them (the loop keeps its time
         # for decoding and applying events), below io_thread_off_rate they
-        # come back. Sampled every 100 ms; switching needs two samples in a row.
+        # come back (requests still in flight are answered on the loop). Sampled
+        # every 100 ms; switching needs two samples in a row.
         self._auto = None
         if settings.pool.io_thread_auto:
             self._auto = self.loop.create_task(self._auto_io_loop())
@@ -322,7 +323,7 @@ class NativeNotifierPool:
             now = c["notify_submitted"]
             rate = (now - last) / period
             last = now
-            want = rate >= on if not self.threaded else not (rate < off and self.core.pending() == 0)
+            want = rate >= on if not self.threaded else rate >= off
             streak = streak + 1 if want != self.threaded else 0
             if streak >= 2:
                 streak = 0

@@ -448,3 +448,40 @@ def test_io_thread_auto_switches_both_ways_without_loss():
         by_uid.setdefault(uid, []).append(name)
     order = {name: i for i, (_u, name) in enumerate(sent)}
     assert all(seq == sorted(seq, key=order.get) for seq in by_uid.values())  # per pod in order
+
+
+def test_io_thread_auto_hands_back_with_requests_in_flight():
+    """The hand-back to the loop does not wait for a quiet queue: requests the
+    thread sent are answered on the loop after the switch, none lost."""
+    import dataclasses
+
+    async def body():
+        sink = StubSink(latency=0.3)  # every response arrives well after the burst ends
+        await sink.start()
+        m = Metrics(record_samples=True)
+        s = settings(sink.url, depth=64, connections=2)
+        s = dataclasses.replace(s, pool=dataclasses.replace(s.pool, io_thread_auto=True, io_thread_on_rate=500.0,
+                                                            io_thread_off_rate=100.0))
+        pool = NativeNotifierPool(s, m)
+        n = 0
+        t_end = time.monotonic() + 0.5
+        while time.monotonic() < t_end:
+            pool.submit(f"u{n}", "ADDED", "default", f"p{n}", core(f"u{n}"), 0, TS)
+            n += 1
+            pool.flush()
+            await asyncio.sleep(0.001)
+        was_threaded = pool.threaded
+        for _ in range(100):  # quiet now: back to the loop while responses are still owed
+            if not pool.threaded:
+                break
+            await asyncio.sleep(0.02)
+        owed_at_switch = pool.outstanding()
+        assert await pool.drain(10)
+        got = len(sink.state.payloads())
+        await close(sink, pool)
+        return n, got, was_threaded, owed_at_switch, m
+
+    n, got, was_threaded, owed, m = run(body(), timeout=60)
+    assert was_threaded and m.c["notify_io_switches"] >= 2
+    assert owed > 0  # the switch really happened with requests in flight
+    assert got == n and m.c["notify_delivered"] == n
