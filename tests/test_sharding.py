@@ -139,13 +139,16 @@ def test_bench_sharded_ranks_exactly_once(ranks):
     assert v["expected"] == v["delivered_by_shards"] > 0
 
 
-def test_bench_single_rank_cluster_watch():
+@pytest.mark.parametrize("step_sync", ["stream", "barrier"])
+def test_bench_single_rank_cluster_watch(step_sync):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
                         "--pods-per-step", "300", "--namespaces", "8", "--ref-events", "200",
-                        "--latency-seconds", "0.5", "--latency-seconds-high", "0.5", "--sink-workers", "1", "--no-placement"],
+                        "--latency-seconds", "0.5", "--latency-seconds-high", "0.5", "--sink-workers", "1", "--no-placement",
+                        "--step-sync", step_sync],
                        capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["step_sync"] == step_sync
     assert d["n_gpus"] == 1 and d["config"]["parallelism"] == "single-process (cluster watch)"
     assert d["per_rank"][0]["events"] == 2 * 1500
     assert d["verify"]["exactly_once"]
