@@ -1,18 +1,16 @@
 #!/usr/bin/env bash
-# GPU-box pass: event->notify latency at 100 and 1,000 ev/s (production
-# profile) for watch reader x thread pinning, alternating, twice.
+# GPU-box A/B of the staging latency curve at high offered load: the current
+# extension vs another build ($PREV_SO, loaded through $K8S_WATCHER_KWCORE_SO),
+# interleaved.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out/lat
+mkdir -p gpurun_out/latab
 for rep in 1 2; do
-  for v in "native auto" "native none" "asyncio auto" "asyncio none"; do
-    set -- $v
-    name="$1-$2-$rep"
-    timeout -k 10 300 python bench.py --steps 3 --warmup 1 --ref-events 0 --latency-seconds 20 --latency-seconds-high 10 \
-      --watch-reader $1 --thread-pinning $2 --json-out gpurun_out/lat/$name.json > gpurun_out/lat/$name.log 2>&1 || { echo "$name failed"; tail -20 gpurun_out/lat/$name.log; exit 1; }
-    python -c "
-import json; d=json.load(open('gpurun_out/lat/$name.json')); h=d['latency_high_rate']
-print('$name', round(d['value']), '| 100/s p50', d['p50_latency_ms'], 'p99', d['p99_latency_ms'], 'n', d['latency_samples'], '| 1k/s p50', h['p50_ms'], 'p90', h['p90_ms'], 'p99', h['p99_ms'], 'n', h['samples'])"
+  for v in prev cur; do
+    if [ $v = prev ]; then export K8S_WATCHER_KWCORE_SO=$PREV_SO; else unset K8S_WATCHER_KWCORE_SO; fi
+    timeout -k 10 300 python -m benchmarks.latency_curve --rates ${RATES:-10000,100000,500000} --ref-rates "" \
+      --out gpurun_out/latab/${v}_$rep.json > gpurun_out/latab/${v}_$rep.md 2> gpurun_out/latab/${v}_$rep.err || { echo "$v failed"; tail -20 gpurun_out/latab/${v}_$rep.err; exit 1; }
+    echo "== $v $rep"; grep -E "^\| [0-9]" gpurun_out/latab/${v}_$rep.md
   done
 done
 echo done
