@@ -66,6 +66,19 @@ def test_reader_hub_on_host():
     test_reader_hub.test_pool_exhaustion_is_backpressure_not_loss()
     test_reader_hub.test_http_stream_adopted_by_hub_end_to_end()
     test_reader_hub.test_read_ahead_is_capped_per_stream()
+    test_reader_hub.test_read_ahead_is_capped_in_bytes_over_all_streams()
+    # the thread recv()s outside its lock: takes and removals racing it, on the host's cores
+    test_reader_hub.test_take_and_remove_race_the_reader_thread()
+
+
+def test_native_sink_on_host(tmp_path):
+    """The bench's native stub clusterapi (_kwcore.SinkServer): pipelined answers, verify keys and
+    the SO_REUSEPORT worker processes' dumps, on the host."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import test_native_sink
+    test_native_sink.test_native_sink_pipelined_answers_and_keys()
+    test_native_sink.test_native_sink_many_connections()
+    test_native_sink.test_sink_process_native_verify_dump(tmp_path)
 
 
 def test_tls_bench_line_is_valid():
