@@ -18,7 +18,7 @@ one notifier flush, which is what keeps Python overhead per event small.
 from __future__ import annotations
 
 import logging
-from typing import List, Optional
+from typing import List, Optional, Tuple
 
 from ..metrics import Metrics
 from ..ops.cache import CORE, MISSING, NAME, NS, PHASE, PodCache, make_pod_cache
@@ -68,7 +68,9 @@ class EventPipeline:
     def attach_native(self, decode_pool=None) -> None:
         """Run watch batches through ``_kwcore.Pipeline`` (decode + this class's
         per-event logic fused in C++), submitting straight into the native
-        notifier core when the pool has one. Relists still use :meth:`reconcile`.
+        notifier core when the pool has one. Relists run natively too
+        (``native.relist``, driven by ``Reflector``); :meth:`reconcile` remains
+        the Python engine's and the WatchList path's.
 
         Line decoding fans out over ``decode_pool`` (a ``_kwcore.DecodePool``
         shared by every scope's pipeline) or, without one, a private pool of
@@ -113,6 +115,43 @@ class EventPipeline:
                 submit(uid, et, ns, name, core, read_ns, ev_ts)
         self.notifier.flush()
         elog.flush()
+        return ctrl
+
+    def native_slice(self, fn, budget_us: float, read_ns: int) -> Tuple[bool, List[tuple]]:
+        """Run one slice of a native relist (``Relist.step`` / ``Relist.sweep``,
+        ``ops/csrc/relist.inc``) and hand its log lines and (asyncio pool)
+        submissions on, as :meth:`handle_raw` does. Returns ``(done, ctrl)``."""
+        log_events = self.log_events
+        flags = (log_events, log_events and self.elog.enabled(logging.DEBUG))
+        if flags != self._native_log:
+            self.native.set_log(*flags)
+            self._native_log = flags
+        done, ctrl, logs, submits = fn(budget_us, read_ns)
+        elog = self.elog
+        if logs:
+            for level, msg in logs:
+                elog.log(level, msg)
+        if submits:
+            submit = self.notifier.submit
+            for uid, et, ns, name, core, ev_ts in submits:
+                submit(uid, et, ns, name, core, read_ns, ev_ts)
+        self.notifier.flush()
+        elog.flush()
+        return done, ctrl
+
+    def delete_scope(self, scope_ns: str, read_ns: int) -> List[tuple]:
+        """Notify every cached pod of namespace ``scope_ns`` as DELETED (from
+        its cached payload) and forget it — what a relist that finds the
+        namespace empty does. Synchronous: a namespace's leftovers are few."""
+        if self.native is None:
+            return self.reconcile([], read_ns, scope_ns=scope_ns)
+        rl = self.native.relist(scope_ns, True)
+        ctrl: List[tuple] = []
+        done = False
+        while not done:
+            done, c = self.native_slice(rl.sweep, 1e9, read_ns)
+            ctrl.extend(c)
+        self.metrics.c["relist_deleted"] += rl.stats()["deleted"]
         return ctrl
 
     def handle_batch(self, events: List[tuple], read_ns: int) -> List[tuple]:

@@ -63,7 +63,8 @@ class WatchListUnsupported(Exception):
 class Reflector:
     def __init__(self, api: KubeApi, settings: Settings, decoder, pipeline: EventPipeline,
                  metrics: Metrics, namespace: Optional[str] = None,
-                 resource_version: Optional[str] = None, primed: bool = False) -> None:
+                 resource_version: Optional[str] = None, primed: bool = False,
+                 list_gate: Optional[asyncio.Semaphore] = None) -> None:
         self.api = api
         self.settings = settings
         self.decoder = decoder
@@ -80,6 +81,11 @@ class Reflector:
         self.synced = asyncio.Event()
         self.watch_count = 0
         self.watch_list = settings.watcher.initial_sync == "watch_list"
+        self.last_relist: Optional[dict] = None  # native relist stats (items, slices, max slice time)
+        # shared by every scope of the service: at most watcher.relist_concurrency
+        # LISTs in flight, so a compaction that expires every namespace watch at
+        # once does not turn into a LIST storm on the API server (or the loop)
+        self.list_gate = list_gate
 
     @property
     def scope(self) -> str:
@@ -99,6 +105,9 @@ class Reflector:
 
     # ------------------------------------------------------------------ list
     async def relist(self, notify: bool = True) -> None:
+        if self.pipeline.native is not None:
+            await self._relist_native(notify)
+            return
         w = self.settings.watcher
         events = []
         cont = None
@@ -136,8 +145,82 @@ class Reflector:
         self.pipeline.last_rv = list_rv
         self.synced.set()
 
+    async def _relist_native(self, notify: bool) -> None:
+        """LIST + reconcile in the native engine (``ops/csrc/relist.inc``).
+
+        Each page is applied as it arrives, in slices of at most
+        ``watcher.relist_slice_ms`` of loop time (the other scopes' watches and
+        the notifier run between them): decode, compare with the cache and
+        notify happen in C++ with no Python object per pod. After the last page
+        the scope's cached pods the LIST lacked are notified DELETED, also in
+        slices. A namespace scope touches only its namespace's cache entries."""
+        w = self.settings.watcher
+        pipe = self.pipeline
+        rl = pipe.native.relist(self.namespace if self._scoped() else None, notify)
+        budget_us = w.relist_slice_ms * 1000.0
+        cont = None
+        list_rv = None
+        limit: Optional[int] = w.list_page_size
+        t_busy = time.monotonic()
+        while True:
+            try:
+                body = await self.api.list_pods_raw(
+                    namespace=self.namespace, limit=limit, continue_token=cont,
+                    label_selector=w.label_selector, field_selector=w.field_selector)
+            except ApiError as exc:
+                if exc.status != 410 or cont is None:
+                    raise
+                # as in relist(): one unpaginated LIST; what the earlier pages
+                # applied stays (a consistent older state), their marks do not
+                self.metrics.c["list_continue_expired"] += 1
+                self.log.warning("LIST continue token expired (410); retrying as one unpaginated LIST")
+                rl.restart()
+                cont, list_rv, limit = None, None, None
+                continue
+            read_ns = time.monotonic_ns()
+            rl.page(body)
+            del body  # the Relist holds the page until its last item is applied
+            while True:
+                done, ctrl = pipe.native_slice(rl.step, budget_us, read_ns)
+                for ev in ctrl:
+                    self._handle_control(ev)
+                if done:
+                    break
+                await asyncio.sleep(0)
+            page_rv, cont = rl.page_meta()
+            if list_rv is None:
+                list_rv = page_rv
+            if not cont:
+                break
+            await asyncio.sleep(0)
+        read_ns = time.monotonic_ns()
+        while True:
+            done, ctrl = pipe.native_slice(rl.sweep, budget_us, read_ns)
+            for ev in ctrl:
+                self._handle_control(ev)
+            if done:
+                break
+            await asyncio.sleep(0)
+        st = rl.stats()
+        c = self.metrics.c
+        c["relists"] += 1
+        c["relist_items"] += st["listed"]
+        c["relist_unchanged"] += st["unchanged"]
+        c["relist_deleted"] += st["deleted"]
+        self.last_relist = dict(st, wall_s=time.monotonic() - t_busy, scope=self.scope)
+        self.rv = list_rv
+        pipe.last_rv = list_rv
+        self.synced.set()
+
     async def sync(self, notify: bool = True) -> None:
         """Initial / post-410 state: WatchList when configured and supported, else LIST."""
+        if self.list_gate is None:
+            await self._sync(notify)
+            return
+        async with self.list_gate:
+            await self._sync(notify)
+
+    async def _sync(self, notify: bool) -> None:
         if self.watch_list:
             try:
                 await self.watch_list_sync(notify)

@@ -114,6 +114,9 @@ class WatcherService:
         self._multi = False  # several (or dynamic) watch scopes, each with its own pipeline
         self.last_checkpoint: Optional[dict] = None
         self._live = False  # scopes follow namespace changes once start() has built the first set
+        self._list_gate: Optional[asyncio.Semaphore] = None  # watcher.relist_concurrency
+        self._ck_lock = asyncio.Lock()  # one checkpoint snapshot+write at a time, in cut order
+        self._ck_inflight: Optional[asyncio.Future] = None  # a format-2 write on its executor thread
 
     # ------------------------------------------------------------------ setup
     def load_endpoint(self) -> KubeEndpoint:
@@ -297,6 +300,11 @@ class WatcherService:
                 self.metrics.gauges["watch_reader_wakeups"] = lambda: float(hub.stats().get("signals", 0))
             self._pin_threads()
         if saved_rvs and None not in scopes:
+            if self.ns_watcher is not None:
+                # namespaces deleted while the watcher was down: their pods get
+                # DELETED from the cache, as _retire_scope and a relist would
+                # (only this shard had them cached: each shard's checkpoint is its own)
+                self._notify_deleted_namespaces(set(self.ns_watcher.names))
             # pods of namespaces this shard no longer watches would never be reconciled
             self._forget_namespaces_except(set(scopes))
         if owed:
@@ -349,8 +357,10 @@ class WatcherService:
             pipe = self._scope_pipeline(dec)
         else:
             dec, pipe = self.decoder, self.pipeline
+        if self._list_gate is None and s.watcher.relist_concurrency > 0:
+            self._list_gate = asyncio.Semaphore(s.watcher.relist_concurrency)
         r = Reflector(self.api, s, dec, pipe, self.metrics, namespace=ns,
-                      resource_version=self._saved_rvs.get(key), primed=primed)
+                      resource_version=self._saved_rvs.get(key), primed=primed, list_gate=self._list_gate)
         if getattr(self.notifier, "saturated", False):
             r.set_paused(True)
         self.reflectors.append(r)
@@ -382,21 +392,29 @@ class WatcherService:
 
     def _forget_namespaces(self, namespaces: Set[str]) -> None:
         """Drop cached pods of namespaces this shard stopped watching, silently:
-        they are now the business of another shard (or gone with the namespace)."""
+        they are now the business of another shard (or gone with the namespace).
+        Both caches index entries by namespace: only those namespaces' pods are touched."""
         cache = self.pipeline.cache if self.pipeline is not None else None
         if cache is None:
             return
-        for uid, ent in cache.items():
-            if ent[2] in namespaces:
-                cache.pop(uid, None)
+        cache.drop_namespaces(namespaces)
 
     def _forget_namespaces_except(self, keep: Set[str]) -> None:
         cache = self.pipeline.cache if self.pipeline is not None else None
         if cache is None:
             return
-        for uid, ent in cache.items():
-            if ent[2] not in keep:
-                cache.pop(uid, None)
+        cache.drop_namespaces_except(keep)
+
+    def _notify_deleted_namespaces(self, existing: Set[str]) -> None:
+        cache = self.pipeline.cache
+        gone = sorted(ns for ns in cache.namespaces() if ns is not None and ns not in existing)
+        for ns in gone:
+            n = cache.count_namespace(ns)
+            self.metrics.c["namespace_deleted_synthesized"] += n
+            self.log.warning(f"Namespace {ns} was deleted while the watcher was down: notifying its "
+                             f"{n} cached pod(s) as DELETED")
+            for ev in self.pipeline.delete_scope(ns, time.monotonic_ns()):
+                self.log.warning(f"Skipping undecodable cached entry ({ev[0]}): {ev[8]}")
 
     def _on_namespaces(self, names: Set[str]) -> None:
         """NamespaceWatcher callback: start/stop reflectors to match the owned set.
@@ -419,7 +437,8 @@ class WatcherService:
             self._start_scope(ns, primed=True)
         for ns in sorted(current - owned):
             if ns not in names:
-                self._retire_scope(ns)
+                if ns not in self._retiring:  # already draining: its timer is running
+                    self._retire_scope(ns)
                 continue
             self.metrics.c["scopes_stopped"] += 1
             self.log.info(f"Stopped watching namespace {ns} (owned by another shard)")
@@ -440,6 +459,9 @@ class WatcherService:
         step = 0.05
         limit = self.settings.watcher.namespace_drain_seconds
         if self._cached_in(ns) and waited < limit:
+            old = self._retiring.get(ns)
+            if old is not None:
+                old.cancel()  # one drain timer per namespace, whoever scheduled it
             self._retiring[ns] = asyncio.get_running_loop().call_later(
                 step, self._retire_scope, ns, waited + step)
             return
@@ -451,7 +473,7 @@ class WatcherService:
             self.metrics.c["namespace_deleted_synthesized"] += n
             self.log.warning(f"Namespace {ns} deleted: {n} pod(s) without a DELETED event after "
                              f"{limit:g}s; notifying them as DELETED from the cache")
-            for ev in pipe.reconcile([], time.monotonic_ns(), scope_ns=ns):
+            for ev in pipe.delete_scope(ns, time.monotonic_ns()):
                 left[0]._handle_control(ev)
         self.metrics.c["scopes_stopped"] += 1
         self.log.info(f"Stopped watching namespace {ns} (deleted)")
@@ -588,6 +610,9 @@ class WatcherService:
                 await self.notifier.close()  # spools the rest
                 closed = drained = True
         if checkpoint and (drained or self._native_checkpoint()):
+            # a periodic write cancelled mid-way keeps running on its thread: let
+            # it land first, so the final cut is the one that stays on disk
+            await self._await_inflight_checkpoint()
             await self._write_checkpoint()  # format 2 carries whatever is still owed
         tasks = list(self._tasks) + list(self._scope_tasks.values())
         for t in tasks:
@@ -647,19 +672,35 @@ class WatcherService:
         ck = self.settings.watcher.checkpoint.path
         if not ck or self.pipeline is None:
             return
-        scopes = {r.scope: r.rv for r in self.reflectors}
-        meta = {"written_at": time.time()}
         if self._native_checkpoint():
-            snap = native_snapshot(self.pipeline.cache, getattr(self.notifier, "core", None))
-            await self._write_snapshot(snap, ck, scopes, meta)
+            await self._write_snapshot(ck)
             return
-        save_checkpoint(ck, scopes, self.pipeline.cache, meta)
+        async with self._ck_lock:
+            scopes = {r.scope: r.rv for r in self.reflectors}
+            save_checkpoint(ck, scopes, self.pipeline.cache, {"written_at": time.time()})
         self.metrics.c["checkpoints_written"] += 1
 
-    async def _write_snapshot(self, snap, ck: str, scopes: dict, meta: dict) -> None:
-        st = snap.stats()
-        loop = asyncio.get_running_loop()
-        nbytes, secs = await loop.run_in_executor(None, write_native, snap, ck, scopes, meta)
+    async def _await_inflight_checkpoint(self) -> None:
+        fut = self._ck_inflight
+        if fut is not None and not fut.done():
+            try:
+                await fut
+            except Exception as exc:  # noqa: BLE001 - the final write below reports its own errors
+                self.log.warning(f"Checkpoint write in progress at shutdown failed: {exc}")
+
+    async def _write_snapshot(self, ck: str) -> None:
+        """Format 2: the consistent cut (a few ms per 100k pods, on the loop
+        thread) and its write (executor thread), one at a time — a later cut is
+        never overwritten by an earlier one."""
+        async with self._ck_lock:
+            await self._await_inflight_checkpoint()
+            scopes = {r.scope: r.rv for r in self.reflectors}
+            meta = {"written_at": time.time()}
+            snap = native_snapshot(self.pipeline.cache, getattr(self.notifier, "core", None))
+            st = snap.stats()
+            loop = asyncio.get_running_loop()
+            self._ck_inflight = loop.run_in_executor(None, write_native, snap, ck, scopes, meta)
+            nbytes, secs = await asyncio.shield(self._ck_inflight)
         g = self.metrics.gauges
         last = {"checkpoint_stall_ms": st["snapshot_seconds"] * 1e3, "checkpoint_write_ms": secs * 1e3,
                 "checkpoint_bytes": float(nbytes), "checkpoint_pods": float(st["entries"]),
@@ -680,9 +721,7 @@ class WatcherService:
             ck = self.settings.watcher.checkpoint.path
             if not ck or self.pipeline is None:
                 return False
-            scopes = {r.scope: r.rv for r in self.reflectors}
-            snap = native_snapshot(self.pipeline.cache, getattr(self.notifier, "core", None))
-            await self._write_snapshot(snap, ck, scopes, {"written_at": time.time()})
+            await self._write_snapshot(ck)
             return True
         for r in self.reflectors:
             r.set_paused(True)

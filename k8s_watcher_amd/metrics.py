@@ -45,6 +45,9 @@ COUNTERS = (
     "api_throttled",        # 429 answers from the API server (not counted against watcher.retry)
     "retry_after_waits",    # retries delayed to the API server's Retry-After
     "relists",
+    "relist_items",         # pods in the LISTs of relists
+    "relist_unchanged",     # ... whose resourceVersion matched the cache (nothing sent)
+    "relist_deleted",       # cached pods a relist no longer found: notified DELETED from the cache
     "list_continue_expired",  # paginated LISTs whose continue token expired (redone unpaginated)
     "watch_list_syncs",     # initial state via WatchList (sendInitialEvents) instead of LIST
     "expired_410",

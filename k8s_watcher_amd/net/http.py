@@ -55,11 +55,23 @@ class Response:
         return 200 <= self.status < 300
 
     def text(self) -> str:
-        return self.body.decode("utf-8", "replace")
+        return bytes(self.body).decode("utf-8", "replace")
 
     def json(self):
         import json
-        return json.loads(self.body)
+        body = self.body
+        return json.loads(body if isinstance(body, (bytes, bytearray)) else bytes(body))
+
+
+def _body_buffer(n: int):
+    """A writable buffer for an ``n``-byte body. Past a few MiB an anonymous
+    mapping: its pages are zero-filled by the kernel as the socket reads touch
+    them, where ``bytearray(n)`` zeroes all of them up front on the loop thread
+    (275 ms for a 400 MB unpaginated LIST of 100k pods)."""
+    if n >= (4 << 20):
+        import mmap
+        return mmap.mmap(-1, n)
+    return bytearray(n)
 
 
 class ResponseParser:
@@ -72,6 +84,7 @@ class ResponseParser:
     """
 
     HEAD, LENGTH, CHUNK_SIZE, CHUNK_DATA, CHUNK_CRLF, TRAILER, UNTIL_CLOSE, DONE, RAW = range(9)
+    DIRECT_MIN = 64 * 1024  # Content-Length bodies this large are read straight into one buffer
 
     def __init__(self) -> None:
         self.reset()
@@ -79,6 +92,12 @@ class ResponseParser:
     def reset(self, no_body: bool = False, raw_chunked: bool = False) -> None:
         self.state = self.HEAD
         self.buf = bytearray()
+        # a large Content-Length body (a LIST page): one buffer of that size,
+        # filled in place — by feed() and, through direct_window(), by the
+        # socket reads themselves — and returned whole by body(): no per-read
+        # bytes objects and no final join
+        self.direct: Optional[bytearray] = None
+        self.direct_off = 0
         self.status = 0
         self.reason = ""
         self.headers: Dict[str, str] = {}
@@ -108,7 +127,22 @@ class ResponseParser:
             self.on_body(parts[0] if len(parts) == 1 else b"".join(parts))
 
     def body(self) -> bytes:
+        if self.direct is not None:
+            return self.direct  # type: ignore[return-value]  (a bytearray: json and the decoder take it)
         return b"".join(self.body_parts)
+
+    def direct_window(self) -> Optional[memoryview]:
+        """Where the next socket read of a direct body goes (None: not in one)."""
+        if self.direct is None or self.state != self.LENGTH or self.buf:
+            return None
+        return memoryview(self.direct)[self.direct_off:]
+
+    def direct_filled(self, n: int) -> None:
+        """``n`` bytes were read into :meth:`direct_window`."""
+        self.direct_off += n
+        self.remaining -= n
+        if self.remaining == 0:
+            self._finish()
 
     def _finish(self) -> None:
         self._flush_body()
@@ -177,6 +211,8 @@ class ResponseParser:
                 pos = idx + 4
                 if self.on_head is not None:
                     self.on_head(self)
+                if self.state == self.LENGTH and self.on_body is None and self.remaining >= self.DIRECT_MIN:
+                    self.direct = _body_buffer(self.remaining)
                 if self.state == self.DONE:
                     self._finish()
                     break
@@ -184,7 +220,11 @@ class ResponseParser:
                 take = min(self.remaining, n - pos)
                 if take <= 0:
                     break
-                self._emit(bytes(buf[pos:pos + take]))
+                if self.direct is not None:
+                    self.direct[self.direct_off:self.direct_off + take] = buf[pos:pos + take]
+                    self.direct_off += take
+                else:
+                    self._emit(bytes(buf[pos:pos + take]))
                 pos += take
                 self.remaining -= take
                 if self.remaining == 0:
@@ -320,6 +360,29 @@ def response_scanner(native: bool = True):
     return PyResponseScanner()
 
 
+_BUF_POOL: Dict[int, List[bytearray]] = {}
+_BUF_POOL_BYTES = [0]
+_BUF_POOL_CAP = 64 << 20
+
+
+def _take_buf(n: int) -> bytearray:
+    """A read buffer of ``n`` bytes: a recycled one if any. Allocating one of
+    256 KiB - 4 MiB means an mmap, zeroed pages and an munmap later — ~0.6 ms
+    of loop time per connection, which a 1,000-namespace relist storm paid
+    thousands of times (benchmarks/relist_storm.py)."""
+    free = _BUF_POOL.get(n)
+    if free:
+        _BUF_POOL_BYTES[0] -= n
+        return free.pop()
+    return bytearray(n)
+
+
+def _give_buf(b: bytearray) -> None:
+    if _BUF_POOL_BYTES[0] + len(b) <= _BUF_POOL_CAP:
+        _BUF_POOL.setdefault(len(b), []).append(b)
+        _BUF_POOL_BYTES[0] += len(b)
+
+
 class _ClientProtocol(asyncio.BufferedProtocol):
     """One TCP/TLS connection; at most one outstanding request (no pipelining here).
 
@@ -336,6 +399,8 @@ class _ClientProtocol(asyncio.BufferedProtocol):
     def __init__(self, loop: asyncio.AbstractEventLoop) -> None:
         self.loop = loop
         self._rbuf: Optional[bytearray] = None
+        self._direct_read = False  # the last get_buffer handed out the parser's direct body window
+        self._want = 65536  # read buffer size now (grows while reads fill it)
         self.zero_copy = False
         self.transport: Optional[asyncio.Transport] = None
         self.parser = ResponseParser()
@@ -359,14 +424,39 @@ class _ClientProtocol(asyncio.BufferedProtocol):
     def connection_made(self, transport) -> None:  # type: ignore[override]
         self.transport = transport
 
-    def get_buffer(self, sizehint: int) -> bytearray:  # type: ignore[override]
+    def get_buffer(self, sizehint: int):  # type: ignore[override]
+        p = self.parser
+        win = p.direct_window()
+        if win is not None:  # a LIST page: read straight into its body buffer
+            self._direct_read = True
+            return win
+        self._direct_read = False
+        # 64 KiB until reads fill it, then 4x per full read up to read_size (a
+        # watch's 4 MiB): a head — all a hub-read watch ever reads here — or a
+        # short reply never allocates the big one
+        want = min(self.read_size, self._want)
         b = self._rbuf
-        if b is None or len(b) != self.read_size:
-            b = self._rbuf = bytearray(self.read_size)  # a fresh one: never resize an exported buffer
+        if b is None or len(b) != want:
+            if b is not None:
+                _give_buf(b)
+            b = self._rbuf = _take_buf(want)
         return b
 
     def buffer_updated(self, nbytes: int) -> None:  # type: ignore[override]
         p = self.parser
+        if self._direct_read:
+            now = time.monotonic_ns()
+            self.read_stamp = now
+            self.last_activity = now * 1e-9
+            try:
+                p.direct_filled(nbytes)
+            except Exception as exc:  # noqa: BLE001
+                self._fail(exc)
+                if self.transport is not None:
+                    self.transport.close()
+            return
+        if nbytes >= len(self._rbuf) and self._want < self.read_size:
+            self._want *= 4  # the socket had more: read more per call from now on
         if self.zero_copy and p.state == ResponseParser.RAW and not p.buf and p.on_body is not None:
             now = time.monotonic_ns()
             self.read_stamp = now
@@ -432,7 +522,9 @@ class _ClientProtocol(asyncio.BufferedProtocol):
 
     def connection_lost(self, exc) -> None:  # type: ignore[override]
         self._unhub()
-        self._rbuf = None  # up to watch_read_bytes (4 MiB) per connection
+        if self._rbuf is not None:  # up to watch_read_bytes (4 MiB): the next connection's
+            _give_buf(self._rbuf)
+            self._rbuf = None
         try:
             self.parser.feed_eof()
         except Exception as err:  # noqa: BLE001

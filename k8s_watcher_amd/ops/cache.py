@@ -77,6 +77,27 @@ class PodCache:
     def count_namespace(self, ns: Optional[str]) -> int:
         return sum(1 for ent in self.entries.values() if ent[NS] == ns)
 
+    def namespaces(self) -> Dict[Optional[str], int]:
+        out: Dict[Optional[str], int] = {}
+        for ent in self.entries.values():
+            out[ent[NS]] = out.get(ent[NS], 0) + 1
+        return out
+
+    def drop_namespaces(self, names) -> int:
+        """Forget every pod of these namespaces; returns how many."""
+        names = set(names)
+        gone = [uid for uid, ent in self.entries.items() if ent[NS] in names]
+        for uid in gone:
+            del self.entries[uid]
+        return len(gone)
+
+    def drop_namespaces_except(self, names) -> int:
+        keep = set(names)
+        gone = [uid for uid, ent in self.entries.items() if ent[NS] not in keep]
+        for uid in gone:
+            del self.entries[uid]
+        return len(gone)
+
     def to_records(self) -> List[list]:
         return [[uid] + ent[:4] + [ent[CORE].decode("utf-8") if ent[CORE] else None]
                 for uid, ent in self.entries.items()]

@@ -1919,6 +1919,7 @@ PyObject* kw_bench_parse(PyObject*, PyObject* args) {
 #include "logsink.inc"
 #include "engine.inc"
 #include "checkpoint.inc"
+#include "relist.inc"
 #include "readerhub.inc"
 #include "sinkserver.inc"
 
@@ -1961,7 +1962,7 @@ PyMODINIT_FUNC PyInit__kwcore(void) {
     Py_INCREF(&ScannerType);
     PyModule_AddObject(m, "ResponseScanner", (PyObject*)&ScannerType);
     if (register_engine(m) < 0 || register_podcache(m) < 0 || register_pipeline(m) < 0 || register_logsink(m) < 0 ||
-        register_checkpoint(m) < 0 || register_readerhub(m) < 0 || register_sinkserver(m) < 0)
+        register_checkpoint(m) < 0 || register_relist(m) < 0 || register_readerhub(m) < 0 || register_sinkserver(m) < 0)
         return nullptr;
     const char* names[6] = {"ADDED", "MODIFIED", "DELETED", "BOOKMARK", "ERROR", "INVALID"};
     for (int i = 0; i < 6; ++i) {

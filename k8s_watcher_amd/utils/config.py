@@ -310,6 +310,8 @@ class WatcherSettings:
     retry: RetryPolicy = field(default_factory=lambda: RetryPolicy(3, 5.0))
     watch_timeout_seconds: int = 300
     list_page_size: int = 500
+    relist_slice_ms: float = 4.0  # native engine: a relist applies its LIST in slices of this much loop time
+    relist_concurrency: int = 16  # scopes LISTing at once (a compaction 410s every namespace watch together); 0 = no cap
     watch_interval: float = 1.0  # accepted for schema parity; a watch has no poll interval
     engine: str = "native"  # native | python
     decode_threads: int = -1  # native engine: extra watch-decode threads, -1 = auto (utils/cpus.py)
@@ -479,6 +481,8 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         retry=_retry(w.get("retry"), "watcher.retry", RetryPolicy(3, 5.0), min_attempts=0),
         watch_timeout_seconds=_as_int(w.get("watch_timeout_seconds", 300), "watcher.watch_timeout_seconds"),
         list_page_size=max(1, _as_int(w.get("list_page_size", 500), "watcher.list_page_size")),
+        relist_slice_ms=_bounded_float(w.get("relist_slice_ms", 4), "watcher.relist_slice_ms", 0.1, 10000.0),
+        relist_concurrency=max(0, _as_int(w.get("relist_concurrency", 16), "watcher.relist_concurrency")),
         watch_interval=_as_float(w.get("watch_interval", 1), "watcher.watch_interval"),
         engine=_choice(w.get("engine", "native"), "watcher.engine", ("native", "python")),
         decode_threads=_decode_threads(w.get("decode_threads", "auto")),

@@ -325,3 +325,102 @@ def test_deleted_namespace_drains_then_synthesizes_deleted(pod_events):
         assert synth == 0 and took < 0.5 + 1.0  # stopped as soon as the pods were gone
     else:
         assert synth == 4 and took >= 0.45
+
+
+def test_recreated_namespace_keeps_its_watch():
+    """A namespace deleted and created again inside the drain window keeps its
+    pod watch, and its live pods are never notified DELETED — even when other
+    namespace changes arrive meanwhile (each used to start a second, untracked
+    drain timer for the draining namespace)."""
+    from k8s_watcher_amd.engine.service import WatcherService
+    from k8s_watcher_amd.kube.kubeconfig import KubeEndpoint
+    from k8s_watcher_amd.metrics import Metrics
+
+    async def body():
+        srv = FakeApiServer(namespaces=["a", "keep"])
+        await srv.start()
+        sink = StubSink()
+        await sink.start()
+        s = load_settings("staging", overrides={
+            "clusterapi": {"base_url": sink.url, "health_check_on_start": False},
+            "watcher": {"namespace_scope": "discover", "namespace_drain_seconds": 0.6,
+                        "retry": {"delay_seconds": 0.05, "max_attempts": 0}}})
+        svc = WatcherService(s, endpoint=KubeEndpoint(server=srv.url), metrics=Metrics())
+        await svc.start()
+        f = PodFactory(seed=4, namespaces=["a"])
+        a_pods = [srv.create(f.new_pod(namespace="a"))["metadata"]["uid"] for _ in range(3)]
+        await sink.state.wait_for(3, timeout=10)
+        # "a" goes away without its pods' DELETED events (they stay cached: the drain waits)
+        srv.deleted_namespaces.add("a")
+        srv._known_ns.discard("a")
+        srv._ns_event("DELETED", "a")
+        await asyncio.sleep(0.1)
+        srv.add_namespace("b")   # another change while "a" drains
+        await asyncio.sleep(0.1)
+        srv.add_namespace("a")   # "a" is back within the drain window
+        await asyncio.sleep(1.2)  # past the drain window
+        watching = any(r.namespace == "a" for r in svc.reflectors)
+        got = collections.Counter((p["uid"], p["event_type"]) for p in sink.state.payloads())
+        synth = svc.metrics.c["namespace_deleted_synthesized"]
+        svc.stop()
+        await svc.shutdown()
+        await sink.stop()
+        await srv.stop()
+        return watching, got, synth, a_pods
+
+    watching, got, synth, a_pods = run(body(), timeout=60)
+    assert watching
+    assert synth == 0
+    assert not any(got[(u, "DELETED")] for u in a_pods)
+
+
+def test_restart_sends_deleted_for_namespaces_deleted_while_down(tmp_path):
+    """discover + checkpoint: a namespace deleted while the watcher was down has
+    its cached pods notified DELETED on restart (as a live deletion or a relist
+    would), instead of being forgotten silently."""
+    from k8s_watcher_amd.engine.service import WatcherService
+    from k8s_watcher_amd.kube.kubeconfig import KubeEndpoint
+    from k8s_watcher_amd.metrics import Metrics
+
+    ck = str(tmp_path / "ck.bin")
+
+    async def body():
+        srv = FakeApiServer(namespaces=["stay", "gone"])
+        await srv.start()
+        sink = StubSink()
+        await sink.start()
+        s = load_settings("staging", overrides={
+            "clusterapi": {"base_url": sink.url, "health_check_on_start": False},
+            "watcher": {"namespace_scope": "discover", "checkpoint": {"path": ck, "interval_seconds": 60},
+                        "retry": {"delay_seconds": 0.05, "max_attempts": 0}}})
+        f = PodFactory(seed=8, namespaces=["stay", "gone"])
+        gone = [srv.create(f.new_pod(namespace="gone"))["metadata"]["uid"] for _ in range(3)]
+        srv.create(f.new_pod(namespace="stay"))
+        svc = WatcherService(s, endpoint=KubeEndpoint(server=srv.url), metrics=Metrics())
+        await svc.start()
+        await sink.state.wait_for(4, timeout=10)
+        svc.stop()
+        await svc.shutdown()  # writes the checkpoint
+        # while down: namespace "gone" and its pods disappear, events compacted away
+        for key in [k for k in srv.pods if k[0] == "gone"]:
+            del srv.pods[key]
+        srv.deleted_namespaces.add("gone")
+        srv._known_ns.discard("gone")
+        svc2 = WatcherService(s, endpoint=KubeEndpoint(server=srv.url), metrics=Metrics())
+        await svc2.start()
+        await sink.state.wait_for(7, timeout=10)
+        await svc2.notifier.drain(5)
+        got = collections.Counter((p["uid"], p["event_type"]) for p in sink.state.payloads())
+        synth = svc2.metrics.c["namespace_deleted_synthesized"]
+        scopes = sorted(r.namespace for r in svc2.reflectors)
+        svc2.stop()
+        await svc2.shutdown()
+        await sink.stop()
+        await srv.stop()
+        return gone, got, synth, scopes
+
+    gone, got, synth, scopes = run(body(), timeout=60)
+    assert scopes == ["stay"]
+    assert synth == 3
+    assert all(got[(u, "DELETED")] == 1 for u in gone)
+    assert sum(got.values()) == 7
