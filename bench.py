@@ -74,7 +74,13 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pods-per-step", type=int, default=10000,
-                    help="pod lifecycles per step PER RANK (5 events each; the cluster has N times as many)")
+                    help="pod lifecycles per churn round PER RANK (5 events each; the cluster has N times as many)")
+    ap.add_argument("--rounds-per-step", type=int, default=24,
+                    help="churn rounds per step: each round re-creates the same --pods-per-step pods (fresh uids), "
+                         "so a step is 24 x 50k events and the driver's 20 timed steps run >= 10 s (sustained)")
+    ap.add_argument("--apart", default="auto", choices=["auto", "on", "off"],
+                    help="after the headline run, measure again with --fixture-placement apart (no latency "
+                         "phases) and report it beside the headline; auto: for N=1 only")
     ap.add_argument("--namespaces", type=int, default=64, help="namespaces in the cluster")
     ap.add_argument("--targets", default="even",
                     help="watcher.namespaces: 'even' (every other namespace), 'all', or a comma list")
@@ -488,12 +494,23 @@ async def rank_main(args, d: Dist) -> dict:
         # at its counter, so some of step k+1's events can already be counted
         target = [c["events_received"]]
         phases: list = []
+        series: list = []  # per whole second of the timed steps: events received (this rank)
+        rss: list = []     # ... and this watcher's RSS (MiB)
+
+        R = max(1, args.rounds_per_step)
+
+        async def send_rounds(k: int) -> list:
+            """Bench step k = fixture steps k*R .. k*R+R-1, back to back."""
+            n = 0
+            for j in range(k * R, k * R + R):
+                n += int((await fx.cmd(f"STEP {j}"))[3])
+            return ["SENT", str(k), "-", str(n)]
 
         async def run_step(k: int, expect: int, pace: str = "") -> None:
             base = target[0]
-            target[0] += expect
+            target[0] += expect * (1 if pace else R)
             t_start = time.perf_counter()
-            sent = asyncio.ensure_future(fx.cmd(f"PACE {k} {pace}" if pace else f"STEP {k}")) \
+            sent = asyncio.ensure_future(fx.cmd(f"PACE {k} {pace}") if pace else send_rounds(k)) \
                 if d.rank == 0 else None
             deadline = time.monotonic() + args.step_timeout
             t_first = t_all = t_sent = None
@@ -527,19 +544,28 @@ async def rank_main(args, d: Dist) -> dict:
             slowest one; the clock still stops only when every event of every
             step is in and every notification is acknowledged."""
             base = target[0]
-            target[0] += expect * steps
+            target[0] += expect * steps * R
             t_start = time.perf_counter()
 
             async def send_all() -> int:
                 n = 0
-                for k in range(k0, k0 + steps):
+                for k in range(k0 * R, (k0 + steps) * R):
                     n += int((await fx.cmd(f"STEP {k}"))[3])
                 return n
 
             sent = asyncio.ensure_future(send_all()) if d.rank == 0 else None
             deadline = time.monotonic() + args.step_timeout * steps
             t_first = t_all = t_sent = None
+            next_tick = t_start + 1.0
+            last_n = base
             while c["events_received"] < target[0] or svc.notifier.outstanding() > 0:
+                now = time.perf_counter()
+                if now >= next_tick:  # events received in each whole second of the timed region
+                    n = c["events_received"]
+                    series.append(n - last_n)
+                    rss.append(_rss_mib())
+                    last_n = n
+                    next_tick += 1.0
                 if t_first is None and c["events_received"] > base:
                     t_first = time.perf_counter()
                 if t_all is None and c["events_received"] >= target[0]:
@@ -611,12 +637,14 @@ async def rank_main(args, d: Dist) -> dict:
 
         # latency at the nominal rate, per rank (untimed)
         metrics.latency.reset()
-        k_lat = args.warmup + args.steps
-        count = max(1, int(args.latency_rate * d.world * args.latency_seconds))
-        count = min(count, shared["events_per_step"])
-        await run_latency(fx, d, svc, c, k_lat, args.latency_rate * d.world, count, args.step_timeout,
-                          notifiable)
-        lat = list(metrics.latency.samples or [])
+        k_lat = (args.warmup + args.steps) * R
+        lat = []
+        if args.latency_seconds > 0:
+            count = max(1, int(args.latency_rate * d.world * args.latency_seconds))
+            count = min(count, shared["events_per_step"])
+            await run_latency(fx, d, svc, c, k_lat, args.latency_rate * d.world, count, args.step_timeout,
+                              notifiable)
+            lat = list(metrics.latency.samples or [])
         # and at 10x that, long enough for >= 5,000 notified samples in the 20%-notifying profile
         lat_hi = []
         if args.latency_rate_high > 0 and args.latency_seconds_high > 0:
@@ -641,7 +669,7 @@ async def rank_main(args, d: Dist) -> dict:
                 verify = await fx.verify_counts()
             if args.ref_events > 0:
                 ref = await run_reference(args, fx, shared, targets, k_lat + 1)
-        return {"elapsed": elapsed, "events": events, "notified": notified,
+        return {"elapsed": elapsed, "events": events, "notified": notified, "series": series, "rss_mib": rss,
                 "events_per_step": shared["events_per_step"], "per_step_mine": per_step, "scopes": len(mine),
                 "lat": lat, "lat_hi": lat_hi, "sat": sat, "failed": failed, "ref": ref, "verify": verify,
                 "delivered_total": delivered_total, "notifiable": notifiable[0],
@@ -679,6 +707,11 @@ async def run_latency(fx, d, svc, c, k: int, rate: float, count: int, timeout: f
             raise TimeoutError(f"rank {d.rank}: latency phase did not drain")
         await asyncio.sleep(0.005)
     await d.abarrier()
+
+
+def _rss_mib() -> float:
+    with open("/proc/self/statm") as fh:
+        return round(int(fh.read().split()[1]) * os.sysconf("SC_PAGE_SIZE") / 2 ** 20, 1)
 
 
 def cpu_snapshot(fx: "Fixtures") -> dict:
@@ -750,6 +783,22 @@ async def run_reference(args, fx: "Fixtures", shared: dict, targets, step: int) 
             "sat_p50_ns": p50}
 
 
+def _sum_series(per_rank: list) -> list:
+    """Per-second event counts summed over ranks (whole seconds every rank saw)."""
+    n = min((len(x) for x in per_rank), default=0)
+    return [sum(x[i] for x in per_rank) for i in range(n)]
+
+
+def _series_stats(series: list):
+    """min / median / max events per second over the timed region's whole seconds."""
+    if not series:
+        return None
+    s = sorted(series)
+    med = s[len(s) // 2]
+    return {"seconds": len(s), "min": s[0], "median": med, "max": s[-1],
+            "min_over_median": round(s[0] / med, 3) if med else None, "per_second": series}
+
+
 def pct(samples, q: float):
     if not samples:
         return None
@@ -770,6 +819,30 @@ def main(argv=None) -> int:
     sat = [x for r in d.all_gather(res["sat"]) for x in r]
     per_rank = d.all_gather({"events": res["events"], "scopes": res["scopes"], "elapsed": round(res["elapsed"], 4),
                              "notified": res["notified"]})
+    series = _sum_series(d.all_gather(res["series"]))
+    rss = d.all_gather(res["rss_mib"])
+    apart = None
+    if args.apart == "on" or (args.apart == "auto" and d.world == 1 and args.fixture_placement != "apart"):
+        # the same timed steps with the API-server fixture and the sink on L3
+        # domains no watcher uses (every socket copy crosses dies): the figure
+        # that does not lean on the fixture sharing the watcher's cache
+        import copy
+        a2 = copy.copy(args)
+        a2.fixture_placement = "apart"
+        a2.latency_seconds = a2.latency_seconds_high = 0.0
+        a2.ref_events = 0
+        a2.warmup = min(args.warmup, 2)
+        a2.steps = max(4, args.steps // 2)
+        r2 = asyncio.run(rank_main(a2, d))
+        el2 = d.reduce(r2["elapsed"], "MAX")
+        ev2 = d.reduce(float(r2["events"]), "SUM")
+        s2 = _sum_series(d.all_gather(r2["series"]))
+        v2 = r2["verify"]
+        apart = {"value": round(ev2 / el2, 1), "steps": a2.steps, "warmup": a2.warmup,
+                 "ms_per_step": round(el2 / a2.steps * 1000, 3), "rate_series": _series_stats(s2),
+                 "exactly_once": (v2["duplicates"] == 0 and v2["unique"] == r2["notifiable"]
+                                  and v2["received"] == r2["notifiable"]) if v2 else None,
+                 "placement_rank0": r2["placement"]}
     d.close()
     if d.rank != 0:
         return 0
@@ -799,8 +872,10 @@ def main(argv=None) -> int:
         "data": "synthetic",
         "config": {
             "model": f"k8s-watcher {args.profile} profile (BASELINE config #4: all-namespaces watch, "
-                     f"{args.pods_per_step}-pod churn per rank, async notifier pool)",
-            "global_batch": int(res["events_per_step"]),
+                     f"{args.pods_per_step}-pod churn per rank x {args.rounds_per_step} rounds per step, "
+                     f"async notifier pool)",
+            "global_batch": int(res["events_per_step"]) * max(1, args.rounds_per_step),
+            "rounds_per_step": max(1, args.rounds_per_step),
             "seq_len": None,
             "parallelism": (f"shard{d.world} (namespace_scope={res['scope']}, "
                             f"{args.namespaces} namespaces, assignment={args.assignment})"
@@ -819,6 +894,10 @@ def main(argv=None) -> int:
         "latency_high_rate": ({"rate_ev_s_per_rank": args.latency_rate_high, "samples": len(lat_hi),
                                "p50_ms": round(pct(lat_hi, 50) / 1e6, 3), "p90_ms": round(pct(lat_hi, 90) / 1e6, 3),
                                "p99_ms": round(pct(lat_hi, 99) / 1e6, 3)} if lat_hi else None),
+        "timed_seconds": round(elapsed, 3),
+        "rate_series": _series_stats(series),
+        "rss_mib_rank0": ({"first": rss[0][0], "last": rss[0][-1], "max": max(rss[0])} if rss and rss[0] else None),
+        "placement_apart": apart,
         "notified_per_s": round(notified / elapsed, 1),
         "notify_failed": res["failed"],
         "verify": verify,
