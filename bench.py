@@ -110,6 +110,8 @@ def parse_args(argv=None):
                          "bytes reach the watcher through that cache (as a NIC's DMA into the LLC would); apart: "
                          "L3 domains no watcher holds — measured 35-40%% slower on the MI355X host "
                          "(profiles/fixture_placement_gpu_box.md): every socket copy crosses dies")
+    ap.add_argument("--validate", default=None, choices=["off", "payload", "full"],
+                    help="watcher.validate (default payload: every raw token copied into a payload checked)")
     ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
     ap.add_argument("--io-thread", action="store_true",
                     help="serve the C++ notifier core's sockets on its own thread (clusterapi.pool.io_thread)")
@@ -443,6 +445,7 @@ async def rank_main(args, d: Dist) -> dict:
                         **({"watch_reader_max_bytes": args.watch_reader_max_bytes}
                            if args.watch_reader_max_bytes is not None else {}),
                         **({"thread_pinning": args.thread_pinning} if args.thread_pinning else {}),
+                        **({"validate": args.validate} if args.validate else {}),
                         # placement already pinned this thread (the decode workers inherit it)
                         **({"decode_affinity": args.decode_affinity or ("none" if watcher_cpus else "auto")})},
         }
@@ -603,6 +606,7 @@ async def rank_main(args, d: Dist) -> dict:
             kw.probe(True)
         dpool = svc._decode_pool or None
         pool0 = dpool.stats() if dpool is not None else None
+        gc_stats = _GcStats()  # collector pauses on the loop thread over the timed steps
         cpu0 = cpu_snapshot(fx)
         t0 = time.perf_counter()
         if prof is not None:
@@ -614,6 +618,7 @@ async def rank_main(args, d: Dist) -> dict:
             for k in range(args.warmup, args.warmup + args.steps):
                 await run_step(k, per_step)
         elapsed = time.perf_counter() - t0
+        gc_report = gc_stats.close()
         step_phases = {key: round(sum(p[key] for p in phases) / len(phases) * 1000, 2) for key in phases[0]} \
             if phases else None
         if prof is not None:
@@ -670,6 +675,7 @@ async def rank_main(args, d: Dist) -> dict:
             if args.ref_events > 0:
                 ref = await run_reference(args, fx, shared, targets, k_lat + 1)
         return {"elapsed": elapsed, "events": events, "notified": notified, "series": series, "rss_mib": rss,
+                "gc": gc_report,
                 "events_per_step": shared["events_per_step"], "per_step_mine": per_step, "scopes": len(mine),
                 "lat": lat, "lat_hi": lat_hi, "sat": sat, "failed": failed, "ref": ref, "verify": verify,
                 "delivered_total": delivered_total, "notifiable": notifiable[0],
@@ -707,6 +713,33 @@ async def run_latency(fx, d, svc, c, k: int, rate: float, count: int, timeout: f
             raise TimeoutError(f"rank {d.rank}: latency phase did not drain")
         await asyncio.sleep(0.005)
     await d.abarrier()
+
+
+class _GcStats:
+    """Python garbage-collector passes (count, total and longest pause per
+    generation) while the timed steps run."""
+
+    def __init__(self) -> None:
+        import gc
+        self.gc = gc
+        self.t0 = 0.0
+        self.stats = {g: [0, 0.0, 0.0] for g in (0, 1, 2)}
+        gc.callbacks.append(self._cb)
+
+    def _cb(self, phase: str, info: dict) -> None:
+        if phase == "start":
+            self.t0 = time.perf_counter()
+        else:
+            dt = time.perf_counter() - self.t0
+            st = self.stats[info["generation"]]
+            st[0] += 1
+            st[1] += dt
+            st[2] = max(st[2], dt)
+
+    def close(self) -> dict:
+        self.gc.callbacks.remove(self._cb)
+        return {f"gen{g}": {"passes": n, "total_ms": round(t * 1e3, 2), "max_ms": round(m * 1e3, 2)}
+                for g, (n, t, m) in self.stats.items()}
 
 
 def _rss_mib() -> float:
@@ -881,6 +914,7 @@ def main(argv=None) -> int:
                             f"{args.namespaces} namespaces, assignment={args.assignment})"
                             if d.world > 1 else f"single-process ({res['scope']} watch)"),
             "engine": args.engine,
+            "validate": args.validate or "payload",
             "decode_threads": res["decode_threads"],
             "clusterapi": "https" if args.tls else "http",
             "api_server": "https" if args.api_tls else "http",
@@ -898,6 +932,7 @@ def main(argv=None) -> int:
         "rate_series": _series_stats(series),
         "rss_mib_rank0": ({"first": rss[0][0], "last": rss[0][-1], "max": max(rss[0])} if rss and rss[0] else None),
         "placement_apart": apart,
+        "gc_rank0": res["gc"],
         "notified_per_s": round(notified / elapsed, 1),
         "notify_failed": res["failed"],
         "verify": verify,

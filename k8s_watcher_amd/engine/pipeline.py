@@ -90,6 +90,8 @@ class EventPipeline:
             w.event_timestamp == "utc", core, False, False, decode)
         if w.payload_extra:
             self.native.set_extra(w.payload_extra)
+        from ..ops.decode import VALIDATE_MODES
+        self.native.set_validate(VALIDATE_MODES[w.validate])
         if self.elog.native_sink is not None:
             self.native.set_log_sink(self.elog.native_sink)  # per-event lines formatted in C++
 

@@ -246,7 +246,7 @@ class WatcherService:
                                                 sp.replay_interval_seconds, sp.replay_batch)
             self._tasks.append(asyncio.ensure_future(self.spool_replayer.run()))
         self.decoder = make_decoder(s.watcher.engine, s.environment, s.watcher.state_format,
-                                    s.watcher.payload_extra)
+                                    s.watcher.payload_extra, s.watcher.validate)
         self._failure = asyncio.get_running_loop().create_future()
         scope_mode = s.watcher.namespace_scope
         if scope_mode == "discover":
@@ -353,7 +353,8 @@ class WatcherService:
         key = ns or "*"
         if self._multi:
             # Each scope decodes its own stream: give it a private decoder.
-            dec = make_decoder(s.watcher.engine, s.environment, s.watcher.state_format, s.watcher.payload_extra)
+            dec = make_decoder(s.watcher.engine, s.environment, s.watcher.state_format, s.watcher.payload_extra,
+                               s.watcher.validate)
             pipe = self._scope_pipeline(dec)
         else:
             dec, pipe = self.decoder, self.pipeline

@@ -478,6 +478,9 @@ bool avx512_supported() {
 #define KEYIS(lit) (kn == sizeof(lit) - 1 && std::memcmp(k, lit, sizeof(lit) - 1) == 0)
 
 void parse_metadata(Parser& P, PodSpans& S) {
+    // a repeated "metadata" key replaces the first one whole (json.loads: the last key wins)
+    S.meta_present = false;
+    S.name = S.ns = S.uid = S.rv = S.labels = S.annotations = S.ctime = S.owners = Span();
     if (P.null_here()) return;
     S.meta_present = true;
     P.object([&](const char* k, size_t kn) {
@@ -509,10 +512,16 @@ void parse_metadata(Parser& P, PodSpans& S) {
     });
 }
 
+// "metadata" present but not an object or null: as absent (the Python engine reads it as {})
+void parse_metadata_absent(PodSpans& S) {
+    S.meta_present = false;
+    S.name = S.ns = S.uid = S.rv = S.labels = S.annotations = S.ctime = S.owners = Span();
+}
+
 void parse_containers(Parser& P, PodSpans& S) {
+    S.containers.clear();  // a repeated key replaces the list (json.loads: the last key wins)
     if (P.null_here()) return;
     if (P.peek() != '[') { P.value(); return; }
-    S.containers.clear();  // duplicate key: last wins
     P.array([&]() {
         if (P.peek() != '{') { P.value(); return; }
         Container c;
@@ -526,9 +535,9 @@ void parse_containers(Parser& P, PodSpans& S) {
 }
 
 void parse_conditions(Parser& P, PodSpans& S) {
+    S.conditions.clear();  // a repeated key replaces the list (json.loads: the last key wins)
     if (P.null_here()) return;
     if (P.peek() != '[') { P.value(); return; }
-    S.conditions.clear();
     P.array([&]() {
         if (P.peek() != '{') { P.value(); return; }
         Condition c;
@@ -544,9 +553,9 @@ void parse_conditions(Parser& P, PodSpans& S) {
 }
 
 void parse_cstatuses(Parser& P, PodSpans& S) {
+    S.cstatuses.clear();  // a repeated key replaces the list (json.loads: the last key wins)
     if (P.null_here()) return;
     if (P.peek() != '[') { P.value(); return; }
-    S.cstatuses.clear();
     P.array([&]() {
         if (P.peek() != '{') { P.value(); return; }
         CStatus c;
@@ -559,6 +568,19 @@ void parse_cstatuses(Parser& P, PodSpans& S) {
         });
         S.cstatuses.push_back(c);
     });
+}
+
+void reset_spec(PodSpans& S) {
+    S.spec_present = false;
+    S.node_name = S.spec_raw = Span();
+    S.containers.clear();
+}
+
+void reset_status(PodSpans& S) {
+    S.status_present = false;
+    S.phase = S.pod_ip = S.host_ip = S.start_time = S.qos = S.cond_raw = S.cstat_raw = Span();
+    S.conditions.clear();
+    S.cstatuses.clear();
 }
 
 void parse_spec(Parser& P, PodSpans& S) {
@@ -604,10 +626,17 @@ void parse_status(Parser& P, PodSpans& S) {
 void parse_pod(Parser& P, PodSpans& S) {
     P.object([&](const char* k, size_t kn) {
         if (KEYIS("metadata")) {
-            if (P.peek() == '{' || P.peek() == 'n') parse_metadata(P, S); else P.value();
+            if (P.peek() == '{' || P.peek() == 'n') {
+                parse_metadata(P, S);
+            } else {
+                P.value();
+                parse_metadata_absent(S);
+            }
         } else if (KEYIS("spec")) {
+            reset_spec(S);
             if (P.peek() == '{' || P.peek() == 'n') parse_spec(P, S); else P.value();
         } else if (KEYIS("status")) {
+            reset_status(S);
             if (P.peek() == '{' || P.peek() == 'n') parse_status(P, S); else P.value();
         } else {
             P.value();
@@ -636,8 +665,14 @@ void parse_pod_light(Parser& P, PodSpans& S) {
     S.deferred = true;
     P.object([&](const char* k, size_t kn) {
         if (KEYIS("metadata")) {
-            if (P.peek() == '{' || P.peek() == 'n') parse_metadata(P, S); else P.value();
+            if (P.peek() == '{' || P.peek() == 'n') {
+                parse_metadata(P, S);
+            } else {
+                P.value();
+                parse_metadata_absent(S);
+            }
         } else if (KEYIS("spec")) {
+            reset_spec(S);
             char c = P.peek();
             if (c == '{') {
                 S.spec_present = true;
@@ -646,6 +681,7 @@ void parse_pod_light(Parser& P, PodSpans& S) {
                 P.value();
             }
         } else if (KEYIS("status")) {
+            reset_status(S);
             if (P.peek() == '{' || P.peek() == 'n') parse_status_light(P, S); else P.value();
         } else {
             P.value();
@@ -881,6 +917,8 @@ void build_core(std::string& o, const PodSpans& S, const std::string& env_json, 
     o.push_back('}');
 }
 
+#include "validate.inc"
+
 // ----------------------------------------------------------------------------- Python glue
 
 PyObject* g_json_loads = nullptr;
@@ -1024,6 +1062,7 @@ struct DecoderObject {
     long long n_events;
     long long n_bytes;
     int extra;  // watcher.payload_extra_fields mask
+    int validate;  // watcher.validate: 0 off, 1 payload (default), 2 full
 };
 
 int hexval(char c);
@@ -1109,6 +1148,12 @@ PyObject* event_tuple(DecoderObject* self, int tidx, PyObject* type_obj, const S
             return t;
         }
     } else {
+        if (self->validate == 1) {  // no malformed sub-tree into a payload (validate.inc)
+            if (const char* why = payload_spans_invalid(S)) {
+                Py_DECREF(t);
+                return make_invalid(why, obj_span.p, obj_span.n);
+            }
+        }
         build_core(*self->out, S, *self->env_json, self->extra);
         PyObject* core = PyBytes_FromStringAndSize(self->out->data(), (Py_ssize_t)self->out->size());
         if (!core) {
@@ -1126,15 +1171,19 @@ PyObject* event_tuple(DecoderObject* self, int tidx, PyObject* type_obj, const S
 PyObject* decode_line(DecoderObject* self, const char* b, size_t n) {
     PodSpans& S = *self->spans;
     S.clear();
+    if (self->validate == 2) {
+        if (const char* why = json_invalid(b, n)) return make_invalid(why, b, n);
+    }
     Span type_span, obj_span;
     try {
-        Parser P(b, b + n);
+        Parser P(b + (has_bom(b, n) ? 3 : 0), b + n);  // as json.loads(bytes): 'utf-8-sig'
         P.object([&](const char* k, size_t kn) {
             if (KEYIS("type")) {
                 type_span = P.value();
             } else if (KEYIS("object")) {
                 if (P.peek() != '{') throw ParseError{"object is not a JSON object"};
                 const char* start = P.p_;
+                S.clear();  // a repeated "object" key: the last one is the pod
                 parse_pod(P, S);
                 obj_span.p = start;
                 obj_span.n = (size_t)(P.p_ - start);
@@ -1208,6 +1257,7 @@ PyObject* Decoder_new(PyTypeObject* type, PyObject*, PyObject*) {
     self->cremain = 0;
     self->n_events = 0;
     self->n_bytes = 0;
+    self->validate = 1;
     return (PyObject*)self;
 }
 
@@ -1403,6 +1453,13 @@ PyObject* Decoder_decode_list(DecoderObject* self, PyObject* arg) {
     if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) < 0) return nullptr;
     const char* b = (const char*)view.buf;
     size_t n = (size_t)view.len;
+    if (self->validate == 2) {
+        if (const char* why = json_invalid(b, n)) {
+            PyBuffer_Release(&view);
+            PyErr_Format(PyExc_ValueError, "invalid list body: %s", why);
+            return nullptr;
+        }
+    }
     PyObject* items = PyList_New(0);
     Span rv, cont;
     bool failed = false;
@@ -1510,6 +1567,17 @@ PyObject* Decoder_core_from_summary(DecoderObject* self, PyObject* args) {
     return PyBytes_FromStringAndSize(self->out->data(), (Py_ssize_t)self->out->size());
 }
 
+PyObject* Decoder_set_validate(DecoderObject* self, PyObject* arg) {
+    long v = PyLong_AsLong(arg);
+    if (PyErr_Occurred()) return nullptr;
+    if (v < 0 || v > 2) {
+        PyErr_SetString(PyExc_ValueError, "validate mode must be 0, 1 or 2");
+        return nullptr;
+    }
+    self->validate = (int)v;
+    Py_RETURN_NONE;
+}
+
 PyObject* Decoder_set_extra(DecoderObject* self, PyObject* arg) {
     self->extra = (int)PyLong_AsLong(arg);
     if (PyErr_Occurred()) return nullptr;
@@ -1522,6 +1590,7 @@ PyObject* Decoder_stats(DecoderObject* self, PyObject*) {
 
 PyMethodDef Decoder_methods[] = {
     {"set_extra", (PyCFunction)Decoder_set_extra, METH_O, "set_extra(mask): watcher.payload_extra_fields"},
+    {"set_validate", (PyCFunction)Decoder_set_validate, METH_O, "set_validate(0 off | 1 payload | 2 full)"},
     {"feed", (PyCFunction)Decoder_feed, METH_O, "feed(bytes) -> list of event tuples"},
     {"feed_chunked", (PyCFunction)Decoder_feed_chunked, METH_O,
      "feed_chunked(bytes) -> events; input keeps its HTTP chunked framing"},
@@ -1923,7 +1992,42 @@ PyObject* kw_bench_parse(PyObject*, PyObject* args) {
 #include "readerhub.inc"
 #include "sinkserver.inc"
 
+// json_invalid(data) -> None if json.loads(data) accepts it, else the reason (validate.inc)
+PyObject* kw_json_invalid(PyObject*, PyObject* arg) {
+    Py_buffer view;
+    if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) < 0) return nullptr;
+    const char* why = json_invalid((const char*)view.buf, (size_t)view.len);
+    PyBuffer_Release(&view);
+    if (!why) Py_RETURN_NONE;
+    return PyUnicode_FromString(why);
+}
+
+// bench_validate(data, repeat) -> seconds: json_invalid over every line of data
+PyObject* kw_bench_validate(PyObject*, PyObject* args) {
+    Py_buffer view;
+    int repeat = 1;
+    if (!PyArg_ParseTuple(args, "y*|i", &view, &repeat)) return nullptr;
+    const char* b = (const char*)view.buf;
+    const char* e = b + view.len;
+    std::vector<std::pair<const char*, size_t>> lines;
+    for (const char* p = b; p < e;) {
+        const char* nl = (const char*)std::memchr(p, '\n', (size_t)(e - p));
+        if (!nl) nl = e;
+        if (nl > p) lines.emplace_back(p, (size_t)(nl - p));
+        p = nl + 1;
+    }
+    size_t bad = 0;
+    const int64_t t0 = mono_ns();
+    for (int r = 0; r < repeat; ++r)
+        for (auto& ln : lines) bad += json_invalid(ln.first, ln.second) != nullptr;
+    const int64_t t1 = mono_ns();
+    PyBuffer_Release(&view);
+    return Py_BuildValue("(dn)", (double)(t1 - t0) * 1e-9, (Py_ssize_t)bad);
+}
+
 PyMethodDef module_methods[] = {
+    {"json_invalid", (PyCFunction)kw_json_invalid, METH_O, "json_invalid(data) -> None | reason (json.loads semantics)"},
+    {"bench_validate", (PyCFunction)kw_bench_validate, METH_VARARGS, "bench_validate(lines, repeat) -> (seconds, invalid)"},
     {"bench_parse", (PyCFunction)kw_bench_parse, METH_VARARGS, "bench_parse(data, mode=2, repeat=1)"},
     {"event_timestamp", (PyCFunction)kw_event_timestamp, METH_O, "event_timestamp(utc) -> str"},
     {"stamp_fields", (PyCFunction)kw_stamp_fields, METH_VARARGS,

@@ -45,8 +45,12 @@ def _s(v: Any) -> Optional[str]:
 def event_from_object(etype: str, obj: Dict[str, Any]) -> tuple:
     if etype == ERROR:
         return (ERROR, None, None, None, None, None, False, None, obj)
-    md = obj.get("metadata") or {}
+    md = obj.get("metadata")
+    if not isinstance(md, dict):  # not an object: absent (as the native engine reads it)
+        md = {}
     st = obj.get("status")
+    if st is not None and not isinstance(st, dict):
+        st = None
     extra = None
     if etype == BOOKMARK:  # True on the WatchList end-of-initial-events marker
         ann = md.get("annotations")
@@ -153,10 +157,15 @@ class PyDecoder:
         return build_core(pod, self.environment, self.state_format, self.extra)
 
 
-def make_decoder(engine: str, environment: str, state_format: str = "structured", extra: int = 0):
+VALIDATE_MODES = {"off": 0, "payload": 1, "full": 2}
+
+
+def make_decoder(engine: str, environment: str, state_format: str = "structured", extra: int = 0,
+                 validate: str = "payload"):
     """``engine="native"`` requires the C++ extension and raises if it is missing.
-    ``extra`` is a :func:`..models.payload.extra_mask`."""
+    ``extra`` is a :func:`..models.payload.extra_mask`; ``validate`` is
+    ``watcher.validate`` (the Python engine always has json.loads' verdict)."""
     if engine == "python" or state_format == "python_repr":
         return PyDecoder(environment, state_format, extra)
     from .native import NativeDecoder
-    return NativeDecoder(environment, state_format, extra)
+    return NativeDecoder(environment, state_format, extra, validate)

@@ -138,11 +138,14 @@ class NativeDecoder:
 
     name = "native"
 
-    def __init__(self, environment: str, state_format: str = "structured", extra: int = 0) -> None:
+    def __init__(self, environment: str, state_format: str = "structured", extra: int = 0,
+                 validate: str = "payload") -> None:
+        from .decode import VALIDATE_MODES
         mod = load()
         d = mod.StreamDecoder(environment, state_format)
         if extra:
             d.set_extra(extra)
+        d.set_validate(VALIDATE_MODES[validate])
         self.extra = extra
         self._d = d
         self.environment = environment

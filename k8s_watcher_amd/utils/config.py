@@ -319,6 +319,10 @@ class WatcherSettings:
     decode_l3_domain: int = -1  # with affinity: index into the host's L3 domains, -1 = the current one
     decode_spin_us: float = 0.0  # idle decode worker spins this long before it sleeps (0 = sleep at once)
     state_format: str = "structured"  # structured | python_repr
+    # native engine: payload (every raw JSON token copied into a payload passes json.loads' rules) |
+    # full (each whole watch line and LIST item must: INVALID exactly when the Python engine's json.loads
+    # fails) | off (bracket matching only)
+    validate: str = "payload"
     event_timestamp: str = "local"  # local | utc
     log_events: Optional[bool] = None  # None = follow log level (parity)
     checkpoint: CheckpointSettings = field(default_factory=CheckpointSettings)
@@ -490,6 +494,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         decode_l3_domain=_as_int(w.get("decode_l3_domain", -1), "watcher.decode_l3_domain"),
         decode_spin_us=_bounded_float(w.get("decode_spin_us", 0), "watcher.decode_spin_us", 0.0, 1e6),
         state_format=_choice(w.get("state_format", "structured"), "watcher.state_format", ("structured", "python_repr")),
+        validate=_choice(w.get("validate", "payload"), "watcher.validate", ("off", "payload", "full")),
         event_timestamp=_choice(w.get("event_timestamp", "local"), "watcher.event_timestamp", ("local", "utc")),
         log_events=None if w.get("log_events") is None else _as_bool(w.get("log_events"), "watcher.log_events"),
         checkpoint=CheckpointSettings(
