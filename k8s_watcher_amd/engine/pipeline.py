@@ -23,7 +23,7 @@ from typing import List, Optional, Tuple
 from ..metrics import Metrics
 from ..ops.cache import CORE, MISSING, NAME, NS, PHASE, PodCache, make_pod_cache
 from ..ops.decode import (ADDED, BOOKMARK, DELETED, E_EXTRA, E_HAS_STATUS, E_NAME, E_NS, E_PHASE,
-                          E_RV, E_TYPE, E_UID, MODIFIED)
+                          E_RV, E_TYPE, E_UID, INVALID, MODIFIED)
 from ..ops.filters import TERMINAL_PHASES
 from ..parallel.shard import ShardFilter
 from ..utils.config import Settings, ShardSettings
@@ -92,6 +92,9 @@ class EventPipeline:
             self.native.set_extra(w.payload_extra)
         from ..ops.decode import VALIDATE_MODES
         self.native.set_validate(VALIDATE_MODES[w.validate])
+        if w.state_format == "python_repr":  # str(V1ContainerState) in C++ (ops/csrc/pyrepr.inc)
+            from ..models.payload import repr_fallback, utc_tzinfo_repr
+            self.native.set_repr(utc_tzinfo_repr(), repr_fallback(self.settings.environment, w.payload_extra))
         if self.elog.native_sink is not None:
             self.native.set_log_sink(self.elog.native_sink)  # per-event lines formatted in C++
 
@@ -210,7 +213,11 @@ class EventPipeline:
                 continue
             core = ev[E_EXTRA]
             if core is None:
-                core = decoder.core(ev)
+                try:
+                    core = decoder.core(ev)
+                except ValueError as exc:  # e.g. a container state the library could not represent
+                    ctrl.append((INVALID, None, None, None, None, None, False, None, f"{exc}"))
+                    continue
             if et != DELETED:
                 set_core(uid, core)
             # stamped per event as it is submitted (reference: at payload build, pod_watcher.py:199)

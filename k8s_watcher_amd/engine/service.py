@@ -541,8 +541,7 @@ class WatcherService:
         self.log.info(f"CPUs {sorted(loop_cpus)} kept for the event-loop thread; {len(tids)} worker threads on the rest")
 
     def _native_pipeline(self) -> bool:
-        w = self.settings.watcher
-        return w.engine == "native" and w.state_format == "structured"
+        return self.settings.watcher.engine == "native"
 
     async def _wait_synced(self) -> None:
         synced = asyncio.ensure_future(asyncio.gather(*[r.synced.wait() for r in self.reflectors]))

@@ -70,20 +70,47 @@ def _lib_datetime(value: Optional[str]):
 
 
 def container_state_repr(state: Dict[str, Any]) -> str:
-    """``str(V1ContainerState(...))`` as the reference sends it."""
+    """``str(V1ContainerState(...))`` as the reference sends it.
+
+    A state (or sub-state) that is not a JSON object is something the
+    library's deserialiser would refuse: ``ValueError`` (the line is INVALID)."""
     from .objects import snake_to_camel
+    if not isinstance(state, dict):
+        raise ValueError("container state is not an object")
     out: Dict[str, Any] = {}
     for sub, attrs in _STATE_SCHEMA.items():
         src = state.get(sub)
         if src is None:
             out[sub] = None
             continue
+        if not isinstance(src, dict):
+            raise ValueError(f"container state {sub!r} is not an object")
         d: Dict[str, Any] = {}
         for a in attrs:
             v = src.get(snake_to_camel(a))
             d[a] = _lib_datetime(v) if a in _STATE_TIME else v
         out[sub] = d
     return pprint.pformat(out)
+
+
+def utc_tzinfo_repr() -> str:
+    """How ``str(V1ContainerState)`` spells a zero UTC offset in this process:
+    ``tzutc()``, or ``tzlocal()`` when the process runs in UTC (dateutil's
+    rule); "" without dateutil (times then stay strings). The native
+    python_repr renderer (``ops/csrc/pyrepr.inc``) is given this."""
+    try:
+        from dateutil import parser as du_parser
+        return repr(du_parser.parse("2025-01-01T00:00:00Z").tzinfo)
+    except Exception:  # noqa: BLE001
+        return ""
+
+
+def repr_fallback(environment: str, extra: int = 0):
+    """object JSON bytes -> python_repr core bytes: what the native engine
+    calls for the (rare) container states it leaves to this module."""
+    def core(obj: bytes) -> bytes:
+        return build_core(json.loads(obj), environment, "python_repr", extra)
+    return core
 
 
 def build_payload_dict(pod: Dict[str, Any], environment: str, state_format: str = "structured",

@@ -825,7 +825,12 @@ void creation_time(std::string& o, const Span& s) {
 
 // extra: bit i = models/payload.py EXTRA_FIELDS[i]
 // (pod_ip, host_ip, start_time, qos_class, resource_version, owner_references)
-void build_core(std::string& o, const PodSpans& S, const std::string& env_json, int extra = 0) {
+bool state_repr_json(std::string& o, const Span& state, const std::string& tz_utc);  // pyrepr.inc
+
+// tz_utc non-null: watcher.state_format python_repr (pyrepr.inc); false when
+// a state needs the Python formatter (the core is then incomplete).
+bool build_core(std::string& o, const PodSpans& S, const std::string& env_json, int extra = 0,
+                const std::string* tz_utc = nullptr) {
     o.clear();
     o.append("{\"name\":");
     raw_or_null(o, S.name);
@@ -865,7 +870,11 @@ void build_core(std::string& o, const PodSpans& S, const std::string& env_json, 
             o.append(",\"restart_count\":");
             raw_or_null(o, c.restart_count);
             o.append(",\"state\":");
-            raw_or_null(o, c.state);
+            if (tz_utc) {
+                if (!state_repr_json(o, c.state, *tz_utc)) return false;
+            } else {
+                raw_or_null(o, c.state);
+            }
             o.push_back('}');
         }
         o.append("]}");
@@ -915,6 +924,7 @@ void build_core(std::string& o, const PodSpans& S, const std::string& env_json, 
         o.push_back('}');
     }
     o.push_back('}');
+    return true;
 }
 
 #include "validate.inc"
@@ -1025,6 +1035,8 @@ PyObject* span_to_str(const Span& s) {
     return PyUnicode_DecodeUTF8(o.data(), (Py_ssize_t)o.size(), "surrogatepass");
 }
 
+#include "pyrepr.inc"
+
 struct InternTable {
     std::unordered_map<std::string, PyObject*> map;
     ~InternTable() {
@@ -1063,6 +1075,8 @@ struct DecoderObject {
     long long n_bytes;
     int extra;  // watcher.payload_extra_fields mask
     int validate;  // watcher.validate: 0 off, 1 payload (default), 2 full
+    std::string* tz_utc;     // state_format python_repr (pyrepr.inc); NULL: structured
+    PyObject* repr_fallback; // object bytes -> core bytes, for states pyrepr.inc leaves to Python
 };
 
 int hexval(char c);
@@ -1154,8 +1168,21 @@ PyObject* event_tuple(DecoderObject* self, int tidx, PyObject* type_obj, const S
                 return make_invalid(why, obj_span.p, obj_span.n);
             }
         }
-        build_core(*self->out, S, *self->env_json, self->extra);
-        PyObject* core = PyBytes_FromStringAndSize(self->out->data(), (Py_ssize_t)self->out->size());
+        PyObject* core;
+        if (build_core(*self->out, S, *self->env_json, self->extra, self->tz_utc)) {
+            core = PyBytes_FromStringAndSize(self->out->data(), (Py_ssize_t)self->out->size());
+        } else {  // a container state the native repr leaves to models/payload.py
+            PyObject* raw = self->repr_fallback ? PyBytes_FromStringAndSize(obj_span.p, (Py_ssize_t)obj_span.n)
+                                                : nullptr;
+            core = raw ? PyObject_CallOneArg(self->repr_fallback, raw) : nullptr;
+            Py_XDECREF(raw);
+            if (!core || !PyBytes_Check(core)) {
+                PyErr_Clear();
+                Py_XDECREF(core);
+                Py_DECREF(t);
+                return make_invalid("container state not representable", obj_span.p, obj_span.n);
+            }
+        }
         if (!core) {
             Py_DECREF(t);
             return nullptr;
@@ -1220,10 +1247,12 @@ int Decoder_init(DecoderObject* self, PyObject* args, PyObject* kwds) {
     Py_ssize_t envn = 0;
     const char* sf = "structured";
     if (!PyArg_ParseTupleAndKeywords(args, kwds, "s#|s", (char**)kwlist, &env, &envn, &sf)) return -1;
-    if (std::strcmp(sf, "structured") != 0) {
-        PyErr_SetString(PyExc_ValueError, "native decoder supports state_format='structured' only");
+    if (std::strcmp(sf, "structured") != 0 && std::strcmp(sf, "python_repr") != 0) {
+        PyErr_SetString(PyExc_ValueError, "state_format must be 'structured' or 'python_repr'");
         return -1;
     }
+    delete self->tz_utc;
+    self->tz_utc = std::strcmp(sf, "python_repr") == 0 ? new std::string("tzutc()") : nullptr;
     // environment as a JSON string literal (via json.dumps for exact escaping)
     PyObject* envs = PyUnicode_FromStringAndSize(env, envn);
     if (!envs) return -1;
@@ -1258,6 +1287,8 @@ PyObject* Decoder_new(PyTypeObject* type, PyObject*, PyObject*) {
     self->n_events = 0;
     self->n_bytes = 0;
     self->validate = 1;
+    self->tz_utc = nullptr;
+    self->repr_fallback = nullptr;
     return (PyObject*)self;
 }
 
@@ -1268,6 +1299,8 @@ void Decoder_dealloc(DecoderObject* self) {
     delete self->spans;
     delete self->interned;
     delete self->chunk_line;
+    delete self->tz_utc;
+    Py_XDECREF(self->repr_fallback);
     Py_TYPE(self)->tp_free((PyObject*)self);
 }
 
@@ -1567,6 +1600,21 @@ PyObject* Decoder_core_from_summary(DecoderObject* self, PyObject* args) {
     return PyBytes_FromStringAndSize(self->out->data(), (Py_ssize_t)self->out->size());
 }
 
+// set_repr(tz_utc_repr, fallback): python_repr details (engine/pipeline.py::repr_settings)
+PyObject* Decoder_set_repr(DecoderObject* self, PyObject* args) {
+    const char* tz;
+    PyObject* fn;
+    if (!PyArg_ParseTuple(args, "sO", &tz, &fn)) return nullptr;
+    if (!self->tz_utc) {
+        PyErr_SetString(PyExc_ValueError, "set_repr: the decoder is not in python_repr mode");
+        return nullptr;
+    }
+    *self->tz_utc = tz;
+    Py_INCREF(fn);
+    Py_XSETREF(self->repr_fallback, fn);
+    Py_RETURN_NONE;
+}
+
 PyObject* Decoder_set_validate(DecoderObject* self, PyObject* arg) {
     long v = PyLong_AsLong(arg);
     if (PyErr_Occurred()) return nullptr;
@@ -1591,6 +1639,7 @@ PyObject* Decoder_stats(DecoderObject* self, PyObject*) {
 PyMethodDef Decoder_methods[] = {
     {"set_extra", (PyCFunction)Decoder_set_extra, METH_O, "set_extra(mask): watcher.payload_extra_fields"},
     {"set_validate", (PyCFunction)Decoder_set_validate, METH_O, "set_validate(0 off | 1 payload | 2 full)"},
+    {"set_repr", (PyCFunction)Decoder_set_repr, METH_VARARGS, "set_repr(tz_utc_repr, fallback): python_repr"},
     {"feed", (PyCFunction)Decoder_feed, METH_O, "feed(bytes) -> list of event tuples"},
     {"feed_chunked", (PyCFunction)Decoder_feed_chunked, METH_O,
      "feed_chunked(bytes) -> events; input keeps its HTTP chunked framing"},

@@ -5,8 +5,7 @@ library (line iteration, ``json.loads``, reflective ``V1Pod`` deserialisation;
 SURVEY §3.2 "Hot loop"). Two engines share one interface:
 
 * :class:`PyDecoder` — stdlib ``json`` + :mod:`..models.payload`; the
-  semantic reference for the native engine and the fallback for
-  ``state_format: python_repr``.
+  semantic reference for the native engine.
 * ``NativeDecoder`` (:mod:`.native`) — C++ single-pass extractor
   (``ops/csrc/kwcore.cpp``) that never builds Python objects for the pod body
   and emits the payload core bytes directly.
@@ -165,7 +164,7 @@ def make_decoder(engine: str, environment: str, state_format: str = "structured"
     """``engine="native"`` requires the C++ extension and raises if it is missing.
     ``extra`` is a :func:`..models.payload.extra_mask`; ``validate`` is
     ``watcher.validate`` (the Python engine always has json.loads' verdict)."""
-    if engine == "python" or state_format == "python_repr":
+    if engine == "python":
         return PyDecoder(environment, state_format, extra)
     from .native import NativeDecoder
     return NativeDecoder(environment, state_format, extra, validate)

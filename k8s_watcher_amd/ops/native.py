@@ -146,6 +146,9 @@ class NativeDecoder:
         if extra:
             d.set_extra(extra)
         d.set_validate(VALIDATE_MODES[validate])
+        if state_format == "python_repr":  # rendered natively (ops/csrc/pyrepr.inc), odd states by Python
+            from ..models.payload import repr_fallback, utc_tzinfo_repr
+            d.set_repr(utc_tzinfo_repr(), repr_fallback(environment, extra))
         self.extra = extra
         self._d = d
         self.environment = environment
