@@ -76,6 +76,38 @@ def slope_mib_per_hour(points: List[Tuple[float, float]]) -> Optional[float]:
     return sum((t - mx) * (v - my) for t, v in points) / sxx * 3600
 
 
+def rss_segments(samples: List[dict], warmup_minutes: float) -> List[dict]:
+    """RSS per watcher process (a SIGKILL restart starts a new one): the
+    in-process slope after that process's own warm-up, so restarts at
+    different RSS levels do not blur the growth rate."""
+    by_pid: Dict[int, List[dict]] = {}
+    for x in samples:
+        if x.get("rss_mb") and x.get("pid"):
+            by_pid.setdefault(x["pid"], []).append(x)
+    out = []
+    for pid, xs in by_pid.items():
+        t0 = xs[0]["t"]
+        after = [x for x in xs if x["t"] - t0 >= warmup_minutes * 60]
+        out.append({"pid": pid, "minutes": round((xs[-1]["t"] - t0) / 60, 1), "samples": len(xs),
+                    "rss_mb_first": xs[0]["rss_mb"], "rss_mb_last": xs[-1]["rss_mb"],
+                    "rss_mb_max": max(x["rss_mb"] for x in xs),
+                    "slope_mib_per_hour_after_warmup": slope_mib_per_hour([(x["t"], x["rss_mb"]) for x in after])})
+    return sorted(out, key=lambda d: -d["minutes"])
+
+
+def memory_at_peak(samples: List[dict]) -> Optional[dict]:
+    """The highest-RSS sample, broken down by what the watcher reports holding."""
+    xs = [x for x in samples if x.get("rss_mb")]
+    if not xs:
+        return None
+    p = max(xs, key=lambda x: x["rss_mb"])
+    mib = lambda k: round((p.get(k) or 0) / 2 ** 20, 1)  # noqa: E731
+    parts = {"cache": mib("cache_bytes"), "notifier_owed": mib("notify_outstanding_bytes"),
+             "watch_read_buffers": mib("watch_reader_allocated_bytes")}
+    return {"t": p["t"], "rss_mb": p["rss_mb"], "accounted_mib": parts,
+            "unaccounted_mib": round(p["rss_mb"] - sum(parts.values()), 1)}
+
+
 class Soak:
     def __init__(self, a) -> None:
         self.a = a
@@ -173,8 +205,9 @@ class Soak:
         m = scrape(self.metrics_port)
         v = vm(self.watcher.pid)
         s = {"t": round(time.monotonic() - self.t0, 1), "step": step, "rss_mb": v.get("VmRSS"),
-             "hwm_mb": v.get("VmHWM")}
+             "hwm_mb": v.get("VmHWM"), "pid": self.watcher.pid}
         for k in ("cached_pods", "cache_bytes", "notify_outstanding", "notify_outstanding_bytes",
+                  "watch_reader_allocated_bytes", "watch_reader_held_bytes",
                   "checkpoint_stall_ms", "checkpoint_write_ms", "checkpoint_bytes", "events_received",
                   "notify_delivered", "expired_410", "watch_restarts", "relists", "bookmarks"):
             if k in m:
@@ -257,7 +290,8 @@ async def amain(a) -> dict:
         while time.monotonic() < end:
             t_step = time.monotonic()
             half = s.E // 2
-            if a.kill_every and step % a.kill_every == 0:
+            in_kill_window = a.kill_window_minutes is None or time.monotonic() - s.t0 < a.kill_window_minutes * 60
+            if a.kill_every and step % a.kill_every == 0 and in_kill_window:
                 s.kinds[step] = "kill"
                 # the last checkpoint (every 5 s) may predate these: re-sent after the restart
                 for back in range(1, int(5.0 / a.step_seconds) + 3):
@@ -318,6 +352,8 @@ async def amain(a) -> dict:
                                     "max": max(x["rss_mb"] for x in after) if after else None,
                                     "slope_mib_per_hour": slope_mib_per_hour([(x["t"], x["rss_mb"]) for x in after])},
             "peak_rss_mb_last_process": last.get("hwm_mb"),
+            "rss_segments": rss_segments(s.samples, a.warmup_minutes),
+            "memory_at_peak": memory_at_peak(s.samples),
             "last_sample": last,
         }
         return {"summary": summary, "samples": s.samples, "verdicts": s.verdicts}
@@ -331,6 +367,8 @@ def main(argv=None) -> int:
     ap.add_argument("--pods", type=int, default=10000)
     ap.add_argument("--step-seconds", type=float, default=5.0)
     ap.add_argument("--kill-every", type=int, default=60, help="SIGKILL the watcher every N steps (0 = never)")
+    ap.add_argument("--kill-window-minutes", type=float, default=None,
+                    help="kills only in the first M minutes; the rest is one process (in-process RSS slope)")
     ap.add_argument("--sample-seconds", type=float, default=10.0)
     ap.add_argument("--warmup-minutes", type=float, default=5.0)
     ap.add_argument("--sink-workers", type=int, default=2)

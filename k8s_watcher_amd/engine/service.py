@@ -298,6 +298,10 @@ class WatcherService:
                 self.metrics.gauges["watch_reader_streams"] = lambda: float(len(hub.protos))
                 self.metrics.gauges["watch_reader_reads"] = lambda: float(hub.stats().get("reads", 0))
                 self.metrics.gauges["watch_reader_wakeups"] = lambda: float(hub.stats().get("signals", 0))
+                # memory accounting: read buffers allocated (up to watch_reader_buffers x watch_read_bytes)
+                self.metrics.gauges["watch_reader_allocated_bytes"] = \
+                    lambda: float(hub.stats().get("allocated_bytes", 0))
+                self.metrics.gauges["watch_reader_held_bytes"] = lambda: float(hub.stats().get("held_bytes", 0))
             self._pin_threads()
         if saved_rvs and None not in scopes:
             if self.ns_watcher is not None:
