@@ -110,6 +110,8 @@ def parse_args(argv=None):
                          "bytes reach the watcher through that cache (as a NIC's DMA into the LLC would); apart: "
                          "L3 domains no watcher holds — measured 35-40%% slower on the MI355X host "
                          "(profiles/fixture_placement_gpu_box.md): every socket copy crosses dies")
+    ap.add_argument("--state-format", default=None, choices=["structured", "python_repr"],
+                    help="watcher.state_format (python_repr: the reference's str(V1ContainerState) text)")
     ap.add_argument("--validate", default=None, choices=["off", "payload", "full"],
                     help="watcher.validate (default payload: every raw token copied into a payload checked)")
     ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
@@ -446,6 +448,7 @@ async def rank_main(args, d: Dist) -> dict:
                            if args.watch_reader_max_bytes is not None else {}),
                         **({"thread_pinning": args.thread_pinning} if args.thread_pinning else {}),
                         **({"validate": args.validate} if args.validate else {}),
+                        **({"state_format": args.state_format} if args.state_format else {}),
                         # placement already pinned this thread (the decode workers inherit it)
                         **({"decode_affinity": args.decode_affinity or ("none" if watcher_cpus else "auto")})},
         }
@@ -915,6 +918,7 @@ def main(argv=None) -> int:
                             if d.world > 1 else f"single-process ({res['scope']} watch)"),
             "engine": args.engine,
             "validate": args.validate or "payload",
+            "state_format": args.state_format or "structured",
             "decode_threads": res["decode_threads"],
             "clusterapi": "https" if args.tls else "http",
             "api_server": "https" if args.api_tls else "http",
