@@ -114,6 +114,8 @@ def parse_args(argv=None):
                     help="watcher.state_format (python_repr: the reference's str(V1ContainerState) text)")
     ap.add_argument("--validate", default=None, choices=["off", "payload", "full"],
                     help="watcher.validate (default payload: every raw token copied into a payload checked)")
+    ap.add_argument("--hub-dispatch", default=None, choices=["on", "off"],
+                    help="watcher.hub_dispatch: hub-read watches feed the native pipeline directly")
     ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
     ap.add_argument("--io-thread", action="store_true",
                     help="serve the C++ notifier core's sockets on its own thread (clusterapi.pool.io_thread)")
@@ -448,6 +450,7 @@ async def rank_main(args, d: Dist) -> dict:
                            if args.watch_reader_max_bytes is not None else {}),
                         **({"thread_pinning": args.thread_pinning} if args.thread_pinning else {}),
                         **({"validate": args.validate} if args.validate else {}),
+                        **({"hub_dispatch": args.hub_dispatch == "on"} if args.hub_dispatch else {}),
                         **({"state_format": args.state_format} if args.state_format else {}),
                         # placement already pinned this thread (the decode workers inherit it)
                         **({"decode_affinity": args.decode_affinity or ("none" if watcher_cpus else "auto")})},
@@ -667,6 +670,7 @@ async def rank_main(args, d: Dist) -> dict:
         delivered_total = c["notify_delivered"]
         hub = getattr(svc, "_reader_hub", None)
         reader = dict(hub.stats(), mode="native") if hub is not None else {"mode": "asyncio"}
+        reader["hub_dispatch_watches"] = c["watches_hub_dispatch"]
         svc.stop()
         await svc.shutdown()
         d.barrier()  # every shard stopped: the sink's counts are final

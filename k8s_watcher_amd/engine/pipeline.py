@@ -107,20 +107,43 @@ class EventPipeline:
         if flags != self._native_log:
             native.set_log(*flags)
             self._native_log = flags
-        ctrl, last_rv, logs, submits, ts = (native.feed_chunked if framed else native.feed)(data, read_ns)
+        ctrl = self.native_result((native.feed_chunked if framed else native.feed)(data, read_ns), read_ns)
+        self.notifier.flush()
+        self.elog.flush()
+        return ctrl
+
+    def native_result(self, res: tuple, read_ns: int) -> List[tuple]:
+        """What Python does with one native feed()'s result — the resume RV,
+        log lines, asyncio-pool submissions — short of flushing (the reader
+        hub's dispatch flushes once for all its streams: :meth:`flush_outputs`).
+        Returns the control events."""
+        ctrl, last_rv, logs, submits, ts = res
         if last_rv is not None:
             self.last_rv = last_rv
-        elog = self.elog
         if logs:
+            elog = self.elog
             for level, msg in logs:
                 elog.log(level, msg)
         if submits:
             submit = self.notifier.submit
             for uid, et, ns, name, core, ev_ts in submits:
                 submit(uid, et, ns, name, core, read_ns, ev_ts)
-        self.notifier.flush()
-        elog.flush()
         return ctrl
+
+    def flush_outputs(self) -> None:
+        """After the reader hub fed bound streams natively: the notifier's and
+        the event log's flush, once, and the log flags the native side uses."""
+        self.sync_native_log()
+        self.notifier.flush()
+        self.elog.flush()
+
+    def sync_native_log(self) -> None:
+        """Hand the event-log switches (log_events, DEBUG on) to the native side."""
+        log_events = self.log_events
+        flags = (log_events, log_events and self.elog.enabled(logging.DEBUG))
+        if flags != self._native_log and self.native is not None:
+            self.native.set_log(*flags)
+            self._native_log = flags
 
     def native_slice(self, fn, budget_us: float, read_ns: int) -> Tuple[bool, List[tuple]]:
         """Run one slice of a native relist (``Relist.step`` / ``Relist.sweep``,

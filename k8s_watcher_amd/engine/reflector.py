@@ -71,7 +71,8 @@ class Reflector:
         self.pipeline = pipeline
         self.metrics = metrics
         self.namespace = namespace
-        self.rv = resource_version
+        self._rv = resource_version
+        self._rv_native = None  # the bound native pipeline's last_rv() while the hub feeds it directly
         self.primed = primed
         self.log = logging.getLogger(SERVICE_LOGGER)
         self.stream = None
@@ -86,6 +87,25 @@ class Reflector:
         # LISTs in flight, so a compaction that expires every namespace watch at
         # once does not turn into a LIST storm on the API server (or the loop)
         self.list_gate = list_gate
+
+    @property
+    def rv(self) -> Optional[str]:
+        """The resume point: the newest resourceVersion seen. While the reader
+        hub feeds the watch to the native pipeline directly
+        (``StreamResponse.bind_native``) no Python runs per read, so it is read
+        from the pipeline."""
+        get = self._rv_native
+        if get is not None:
+            v = get()
+            if v is not None:
+                return v
+        return self._rv
+
+    @rv.setter
+    def rv(self, value: Optional[str]) -> None:
+        self._rv = value
+        if self._rv_native is not None:
+            self.pipeline.native.set_last_rv(value)
 
     @property
     def scope(self) -> str:
@@ -379,7 +399,15 @@ class Reflector:
                 for ev in ctrl:
                     self._handle_control(ev)
 
+        def on_native(res: tuple, read_ns: int, body_done: bool) -> None:
+            for ev in pipeline.native_result(res, read_ns):
+                self._handle_control(ev)
+            if body_done and self.stream is not None:
+                self.stream.close()  # server ended the watch (timeoutSeconds)
+
         pipeline.last_rv = self.rv
+        if native is not None:
+            native.set_last_rv(self.rv)
         self.stream = await self.api.watch_pods(
             sink, namespace=self.namespace, resource_version=self.rv,
             timeout_seconds=w.watch_timeout_seconds or None, allow_bookmarks=True,
@@ -388,6 +416,12 @@ class Reflector:
             zero_copy=native is not None)  # the fused pipeline copies what it keeps (partial lines)
         self.watch_count += 1
         self.connected.set()
+        if (native is not None and framed[0] and w.hub_dispatch
+                and self.stream.bind_native(native, on_native, pipeline.flush_outputs,
+                                            (id(pipeline.notifier), id(pipeline.elog)))):
+            self._rv_native = native.last_rv
+            pipeline.sync_native_log()
+            self.metrics.c["watches_hub_dispatch"] += 1
         if self._stop.is_set():
             self.stream.close()
         if self._paused:
@@ -405,6 +439,10 @@ class Reflector:
         finally:
             self.stream.close()
             self.stream = None
+            if self._rv_native is not None:
+                self._rv = self.rv
+                self._rv_native = None
+                pipeline.last_rv = self._rv
         if self._expired:
             raise Expired()
         if self._error:

@@ -48,6 +48,7 @@ COUNTERS = (
     "relist_items",         # pods in the LISTs of relists
     "relist_unchanged",     # ... whose resourceVersion matched the cache (nothing sent)
     "relist_deleted",       # cached pods a relist no longer found: notified DELETED from the cache
+    "watches_hub_dispatch",  # watches the reader hub fed to the native pipeline directly (hub_dispatch)
     "list_continue_expired",  # paginated LISTs whose continue token expired (redone unpaginated)
     "watch_list_syncs",     # initial state via WatchList (sendInitialEvents) instead of LIST
     "expired_410",

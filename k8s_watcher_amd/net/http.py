@@ -413,6 +413,7 @@ class _ClientProtocol(asyncio.BufferedProtocol):
         self.read_stamp = 0
         self.hub = None  # net/reader.WatchReaderHub that reads this socket, once adopted
         self.hub_sid = 0
+        self.hub_result: Optional[Callable[[tuple, int, bool], None]] = None  # bind_native
 
     def deliver(self, data: bytes) -> None:
         """``parser.on_body`` for streams: body bytes + the socket-read timestamp."""
@@ -494,6 +495,23 @@ class _ClientProtocol(asyncio.BufferedProtocol):
         except Exception as exc:  # noqa: BLE001
             self._fail(exc)
             self.close()
+
+    def hub_native(self, result, read_ns: int, body_done: bool) -> None:
+        """A read the hub fed to a bound native pipeline needs Python
+        (:meth:`StreamResponse.bind_native`): ``result`` is the pipeline's
+        feed() tuple, or the exception it raised."""
+        self.read_stamp = read_ns
+        if isinstance(result, BaseException):
+            self._fail(result)
+            self.close()
+            return
+        cb = self.hub_result
+        if cb is not None:
+            try:
+                cb(result, read_ns, body_done)
+            except Exception as exc:  # noqa: BLE001  (as a sink raising in hub_data)
+                self._fail(exc)
+                self.close()
 
     def hub_eof(self, err: int) -> None:
         """The hub saw the peer close (err 0) or the socket / TLS session fail:
@@ -578,8 +596,24 @@ class StreamResponse:
     def last_activity(self) -> float:
         return self._proto.last_activity
 
+    def bind_native(self, pipeline_core, on_result, flush, flush_key) -> bool:
+        """A hub-read watch body (net/reader.py) goes straight from the hub's
+        buffers into the fused native ``pipeline_core`` — no Python call per
+        socket read; ``on_result(result, read_ns, body_done)`` gets only the
+        reads that need Python. False (nothing changed) when the stream is
+        not hub-read or not at a clean pass-through point."""
+        p = self._proto
+        hub = p.hub
+        parser = p.parser
+        if (hub is None or parser.state != ResponseParser.RAW or parser.buf or p.stream_sink is None
+                or p.closed.done()):
+            return False
+        hub.bind(p, pipeline_core, parser.raw_chunked, on_result, flush, flush_key)
+        return p.hub_result is not None
+
     def close(self) -> None:
         self._proto.stream_sink = None
+        self._proto.hub_result = None
         self._proto.close()
 
 

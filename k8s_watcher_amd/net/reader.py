@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import asyncio
 import os
+import time
 from typing import Dict, Optional
 
 from ..ops import native
@@ -41,6 +42,7 @@ class WatchReaderHub:
                                             max(0, int(max_bytes)))
         self.protos: Dict[int, object] = {}
         self._tls: Dict[tuple, object] = {}
+        self._flush: Dict[object, object] = {}  # bind(): once per dispatch
         self._fd = self.core.fileno()
         self.loop.add_reader(self._fd, self._on_ready)
         self.closed = False
@@ -83,6 +85,20 @@ class WatchReaderHub:
     def error_text(self, sid: int) -> str:
         return "" if self.closed else self.core.error_text(sid)
 
+    def bind(self, proto, pipeline_core, framed: bool, on_result, flush, flush_key) -> None:
+        """Feed ``proto``'s body straight to a fused ``_kwcore.Pipeline`` on
+        the hub's dispatch (no Python call per read): only reads whose result
+        needs Python — control events, log lines, submissions, the end of the
+        body, an error — come back, through ``on_result(result, read_ns,
+        body_done)``. ``flush`` runs once per dispatch that fed a bound stream
+        (one per distinct ``flush_key``: streams sharing a notifier flush it
+        once)."""
+        if self.closed or proto.hub is not self:
+            return
+        self.core.bind(proto.hub_sid, pipeline_core, framed)
+        proto.hub_result = on_result
+        self._flush[flush_key] = flush
+
     def forget(self, sid: int) -> None:
         if self.protos.pop(sid, None) is not None and not self.closed:
             self.core.remove(sid)
@@ -93,7 +109,28 @@ class WatchReaderHub:
 
     def _on_ready(self) -> None:
         core = self.core
-        for sid, buf, view, read_ns, err in core.take():
+        items, touched = core.take_dispatch()
+        protos = self.protos
+        if touched:
+            now = time.monotonic()
+            for sid in touched:
+                proto = protos.get(sid)
+                if proto is not None:
+                    proto.last_activity = now
+        try:
+            self._deliver(core, items)
+        finally:
+            if touched:
+                for flush in list(self._flush.values()):
+                    flush()
+
+    def _deliver(self, core, items) -> None:
+        for sid, buf, view, read_ns, err in items:
+            if buf == -2:  # a bound stream's read that needs Python (take_dispatch)
+                proto = self.protos.get(sid)
+                if proto is not None:
+                    proto.hub_native(view, read_ns, bool(err))
+                continue
             try:
                 proto = self.protos.get(sid)
                 if proto is not None:
@@ -125,6 +162,7 @@ class WatchReaderHub:
             proto.hub = None
             proto.close()
         self.protos.clear()
+        self._flush.clear()
         self.core.close()
 
 

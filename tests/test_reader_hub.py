@@ -331,3 +331,93 @@ def test_take_and_remove_race_the_reader_thread():
         t.join(10)
     for a, _b in pairs:
         a.close()
+
+
+def _chunked(data: bytes, piece: int = 7000) -> bytes:
+    out = bytearray()
+    for i in range(0, len(data), piece):
+        part = data[i:i + piece]
+        out += b"%x\r\n" % len(part) + part + b"\r\n"
+    return bytes(out + b"0\r\n\r\n")
+
+
+def _dispatch_until(core, pred, on_item, timeout=10.0):
+    deadline = time.monotonic() + timeout
+    touched_all = set()
+    while not pred() and time.monotonic() < deadline:
+        items, touched = core.take_dispatch()
+        touched_all.update(touched)
+        for it in items:
+            on_item(it)
+        time.sleep(0.001)
+    return touched_all
+
+
+@pytest.mark.parametrize("ov", [{}, {"watcher": {"namespaces": ["none-of-these"]}}])
+def test_take_dispatch_feeds_bound_pipeline_like_handle_raw(ov):
+    """A stream bound to a native Pipeline is fed by take_dispatch itself: the
+    submits, cache, resume RV and control events equal handle_raw's on the
+    same bytes, only reads that need Python come back, an unbound stream on
+    the same hub still gets its raw buffers, and the end of the body is
+    reported once."""
+    from test_native_pipeline import Recorder, run_native, stream
+    from k8s_watcher_amd.engine.pipeline import EventPipeline
+    from k8s_watcher_amd.metrics import Metrics
+    from k8s_watcher_amd.ops.decode import PyDecoder
+    from k8s_watcher_amd.utils.config import load_settings
+
+    data = stream()
+    want_calls, want_cache, _, want_rv, want_ctrl = run_native("production", ov, data)
+    s = load_settings("production", overrides=ov, environ={})
+    rec = Recorder()
+    p = EventPipeline(s, PyDecoder("production"), rec, Metrics())
+    p.log_events_setting = False
+    p.attach_native()
+    p.sync_native_log()
+    core = load().ReaderHub(16 * 1024, 8)  # small buffers: many reads, lines split across them
+    (a, b), (c, d) = socket.socketpair(), socket.socketpair()
+    bound, plain = core.add(os.dup(b.fileno())), core.add(os.dup(d.fileno()))
+    core.bind(bound, p.native, True)
+    raw = _chunked(data)
+    import threading
+    sender = threading.Thread(target=a.sendall, args=(raw,), daemon=True)  # the hub's small pool fills: send meanwhile
+    sender.start()
+    c.sendall(b"plain bytes")
+    c.shutdown(socket.SHUT_WR)
+    ctrl, plain_got, done, attention = [], bytearray(), [], [0]
+
+    def on_item(it):
+        sid, buf, view, read_ns, err = it
+        if buf == -2:
+            assert sid == bound and not isinstance(view, BaseException)
+            attention[0] += 1
+            ctrl.extend(e[0] for e in p.native_result(view, read_ns))
+            if err:
+                done.append(sid)
+            return
+        if view is None:
+            return
+        if sid == bound:  # after one that needed Python in the same batch: the sink's path
+            ctrl.extend(e[0] for e in p.native_result(p.native.feed_chunked(view, read_ns), read_ns))
+            if p.native.body_done():
+                done.append(sid)
+        else:
+            plain_got.extend(view)
+        view.release()
+        core.release(buf)
+
+    touched = _dispatch_until(core, lambda: done and plain_got == b"plain bytes", on_item)
+    sender.join()
+    assert done == [bound] and bytes(plain_got) == b"plain bytes"
+    assert {bound, plain} <= touched
+    assert rec.calls == want_calls
+    assert {u: list(e) for u, e in p.cache.items()} == {u: list(e) for u, e in want_cache.items()}
+    assert ctrl == want_ctrl and "ERROR" in ctrl
+    assert p.native.last_rv() == want_rv
+    stats = core.stats()
+    if not want_calls:  # nothing to submit: only the control events and the end came back
+        assert attention[0] <= len(want_ctrl) + 1 < stats["reads"]
+    core.unbind(bound)
+    core.close()
+    for x in (a, b, c, d):
+        x.close()

@@ -152,6 +152,7 @@ def test_bench_single_rank_cluster_watch(step_sync):
     assert d["n_gpus"] == 1 and d["config"]["parallelism"] == "single-process (cluster watch)"
     assert d["per_rank"][0]["events"] == 2 * 1500
     assert d["verify"]["exactly_once"]
+    assert d["watch_reader_rank0"]["hub_dispatch_watches"] >= 1
     assert d["reference_equiv"]["events"] == 200 and d["vs_baseline"] > 0
 
 
@@ -166,6 +167,7 @@ def test_bench_https_api_server_through_the_native_reader():
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert d["config"]["api_server"] == "https" and d["verify"]["exactly_once"]
     assert d["watch_reader_rank0"]["mode"] == "native" and d["watch_reader_rank0"]["reads"] > 0
+    assert d["watch_reader_rank0"]["hub_dispatch_watches"] > 0  # TLS watches are fed natively too
     assert d["per_rank"][0]["events"] == 2 * 1500
 
 
