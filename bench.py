@@ -81,6 +81,12 @@ def parse_args(argv=None):
     ap.add_argument("--apart", default="auto", choices=["auto", "on", "off"],
                     help="after the headline run, measure again with --fixture-placement apart (no latency "
                          "phases) and report it beside the headline; auto: for N=1 only")
+    ap.add_argument("--staging", default="auto", choices=["auto", "on", "off"],
+                    help="also run the staging profile (every event notified): its saturated notification rate "
+                         "and p50/p99 at --staging-latency-rate (auto: after a production run)")
+    ap.add_argument("--staging-steps", type=int, default=4, help="timed steps of the staging phase")
+    ap.add_argument("--staging-latency-rate", type=float, default=100000.0,
+                    help="ev/s over the whole job for the staging phase's latency figure")
     ap.add_argument("--namespaces", type=int, default=64, help="namespaces in the cluster")
     ap.add_argument("--targets", default="even",
                     help="watcher.namespaces: 'even' (every other namespace), 'all', or a comma list")
@@ -883,6 +889,41 @@ def main(argv=None) -> int:
                  "exactly_once": (v2["duplicates"] == 0 and v2["unique"] == r2["notifiable"]
                                   and v2["received"] == r2["notifiable"]) if v2 else None,
                  "placement_rank0": r2["placement"]}
+    staging = None
+    if args.staging == "on" or (args.staging == "auto" and args.profile == "production"):
+        # BASELINE configs #2/#3: every event notified (the staging profile) —
+        # the saturated notification rate, then p50/p99 at a fixed offered rate
+        import copy
+        a3 = copy.copy(args)
+        a3.profile = "staging"
+        a3.targets = "all"  # every event of the replay is one notification
+        a3.latency_seconds = 0.0
+        a3.latency_rate_high = args.staging_latency_rate / d.world
+        a3.latency_seconds_high = 1.0  # capped at one fixture step of events per rank
+        a3.ref_events = 0
+        a3.probe = False
+        a3.warmup = 1
+        a3.steps = max(1, args.staging_steps)
+        a3.fixture_placement = args.fixture_placement
+        r3 = asyncio.run(rank_main(a3, d))
+        el3 = d.reduce(r3["elapsed"], "MAX")
+        ev3 = d.reduce(float(r3["events"]), "SUM")
+        nt3 = d.reduce(float(r3["notified"]), "SUM")
+        dl3 = d.reduce(float(r3["delivered_total"]), "SUM")
+        fl3 = d.reduce(float(r3["failed"]), "SUM")
+        s3 = _sum_series(d.all_gather(r3["series"]))
+        lat3 = [x for r in d.all_gather(r3["lat_hi"]) for x in r]
+        v3 = r3["verify"]
+        staging = {"profile": "staging", "every_event_notified_per_s": round(nt3 / el3, 1),
+                   "events_per_s": round(ev3 / el3, 1), "steps": a3.steps, "warmup": a3.warmup,
+                   "timed_seconds": round(el3, 3), "ms_per_step": round(el3 / a3.steps * 1000, 3),
+                   "rate_series": _series_stats(s3), "notify_failed": int(fl3),
+                   "latency_rate_ev_s": args.staging_latency_rate, "latency_samples": len(lat3),
+                   "p50_latency_ms": round(pct(lat3, 50) / 1e6, 3) if lat3 else None,
+                   "p99_latency_ms": round(pct(lat3, 99) / 1e6, 3) if lat3 else None,
+                   "exactly_once": (v3["duplicates"] == 0 and v3["unique"] == r3["notifiable"]
+                                    and v3["received"] == r3["notifiable"]) if v3 else None,
+                   "delivered_by_shards": int(dl3), "cpu_util_rank0": r3["cpu_util"]}
     d.close()
     if d.rank != 0:
         return 0
@@ -940,6 +981,7 @@ def main(argv=None) -> int:
         "rate_series": _series_stats(series),
         "rss_mib_rank0": ({"first": rss[0][0], "last": rss[0][-1], "max": max(rss[0])} if rss and rss[0] else None),
         "placement_apart": apart,
+        "staging": staging,
         "gc_rank0": res["gc"],
         "notified_per_s": round(notified / elapsed, 1),
         "notify_failed": res["failed"],

@@ -31,7 +31,7 @@ def test_smoke_end_to_end():
 
 
 def test_bench_line_is_valid():
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off",
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off",
                           "--pods-per-step", "1000", "--ref-events", "500", "--latency-seconds", "1", "--latency-seconds-high", "1"],
                          capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
@@ -47,7 +47,7 @@ def test_bench_line_is_valid():
 
 def test_https_api_server_bench_line_is_valid():
     """An https API server (every real cluster) through the hub's native TLS on the host."""
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off",
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off",
                           "--pods-per-step", "1000", "--ref-events", "0", "--latency-seconds", "1",
                           "--latency-rate-high", "0", "--api-tls"],
                          capture_output=True, text=True, timeout=600, cwd=ROOT)
@@ -83,7 +83,7 @@ def test_native_sink_on_host(tmp_path):
 
 def test_tls_bench_line_is_valid():
     """production.yaml's https clusterapi through the native TLS notifier core, on the host."""
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off",
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off",
                           "--pods-per-step", "1000", "--ref-events", "0", "--latency-seconds", "1", "--latency-rate-high", "0", "--tls"],
                          capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]

@@ -117,7 +117,7 @@ def test_bench_sharded_ranks_exactly_once(ranks):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", BENCH_DEBUG="1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-                        "--gpus", str(ranks), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--pods-per-step", "300",
+                        "--gpus", str(ranks), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off", "--pods-per-step", "300",
                         "--namespaces", "16", "--ref-events", "0", "--latency-seconds", "0.5", "--latency-seconds-high", "0.5",
                         "--sink-workers", "2", "--fixture-workers", "2", "--no-placement",
                         "--decode-threads", "0", "--step-timeout", "45"],
@@ -141,7 +141,7 @@ def test_bench_sharded_ranks_exactly_once(ranks):
 
 @pytest.mark.parametrize("step_sync", ["stream", "barrier"])
 def test_bench_single_rank_cluster_watch(step_sync):
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off",
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off",
                         "--pods-per-step", "300", "--namespaces", "8", "--ref-events", "200",
                         "--latency-seconds", "0.5", "--latency-seconds-high", "0.5", "--sink-workers", "1", "--no-placement",
                         "--step-sync", step_sync],
@@ -159,7 +159,7 @@ def test_bench_single_rank_cluster_watch(step_sync):
 def test_bench_https_api_server_through_the_native_reader():
     """bench.py --api-tls: the replay API server speaks TLS (as every real
     cluster does) and the watcher's hub runs the session natively."""
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off",
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off",
                         "--pods-per-step", "300", "--namespaces", "8", "--ref-events", "0", "--api-tls",
                         "--latency-seconds", "0.5", "--latency-seconds-high", "0.5", "--sink-workers", "1", "--no-placement"],
                        capture_output=True, text=True, timeout=600, cwd=ROOT)
@@ -430,10 +430,13 @@ def test_restart_sends_deleted_for_namespaces_deleted_while_down(tmp_path):
 
 def test_bench_sustained_rounds_and_apart_placement():
     """The headline's shape: each step is several churn rounds (a sustained
-    window), the per-second rate series is reported, and a second run with the
-    fixtures placed apart is reported beside it — both exactly-once."""
+    window), the per-second rate series is reported, a second run with the
+    fixtures placed apart is reported beside it, and a staging-profile run
+    (every event notified: saturated rate, p99 at a fixed rate) — all
+    exactly-once."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
                         "--rounds-per-step", "3", "--apart", "on", "--pods-per-step", "300", "--namespaces", "8",
+                        "--staging-steps", "2", "--staging-latency-rate", "2000",
                         "--ref-events", "0", "--latency-seconds", "0.5", "--latency-seconds-high", "0",
                         "--sink-workers", "1", "--no-placement"],
                        capture_output=True, text=True, timeout=600, cwd=ROOT)
@@ -447,3 +450,8 @@ def test_bench_sustained_rounds_and_apart_placement():
     assert rs is None or (rs["min"] <= rs["median"] <= rs["max"] and len(rs["per_second"]) == rs["seconds"])
     a = d["placement_apart"]
     assert a["exactly_once"] and a["value"] > 0 and a["steps"] == 4
+    st = d["staging"]
+    assert st["profile"] == "staging" and st["exactly_once"] and st["steps"] == 2
+    # every event of the timed steps is notified (the staging profile filters nothing)
+    assert st["every_event_notified_per_s"] == pytest.approx(st["events_per_s"], rel=0.02)
+    assert st["latency_samples"] > 0 and st["p99_latency_ms"] >= st["p50_latency_ms"] > 0
