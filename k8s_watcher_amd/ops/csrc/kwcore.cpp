@@ -38,6 +38,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <charconv>
 #include <atomic>
 #include <cctype>
 #include <cerrno>
@@ -2013,9 +2014,10 @@ PyObject* kw_bench_parse(PyObject*, PyObject* args) {
                         P.value();
                     }
                 });
-                if (mode == 2 || mode == 4) {
+                if (mode == 2 || mode == 4 || mode == 5) {
+                    static const std::string tz_utc = "tzutc()";
                     materialize(S);
-                    build_core(out, S, env);
+                    build_core(out, S, env, 0, mode == 5 ? &tz_utc : nullptr);  // 5: state_format python_repr
                     sink += out.size();
                 } else {
                     sink += S.name.n;
