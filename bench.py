@@ -87,6 +87,10 @@ def parse_args(argv=None):
     ap.add_argument("--staging-steps", type=int, default=4, help="timed steps of the staging phase")
     ap.add_argument("--staging-latency-rate", type=float, default=100000.0,
                     help="ev/s over the whole job for the staging phase's latency figure")
+    ap.add_argument("--soak-minutes", type=float, default=0.0,
+                    help="instead of the timed steps: stream steps back to back for this long, checking "
+                         "exactly-once and sampling RSS every --soak-chunk-steps steps (prints a soak JSON line)")
+    ap.add_argument("--soak-chunk-steps", type=int, default=10)
     ap.add_argument("--namespaces", type=int, default=64, help="namespaces in the cluster")
     ap.add_argument("--targets", default="even",
                     help="watcher.namespaces: 'even' (every other namespace), 'all', or a comma list")
@@ -348,12 +352,13 @@ class Fixtures:
         await self.replay.stdin.drain()
         return (await self.replay.stdout.readline()).decode().split()
 
-    async def verify_counts(self) -> dict:
-        """Snapshot of the sink's key counts over all its workers (SIGUSR1)."""
+    async def verify_counts(self, reset: bool = False) -> dict:
+        """Snapshot of the sink's key counts over all its workers (SIGUSR1;
+        SIGUSR2 also clears them, so a long run does not grow the sink)."""
         for f in glob.glob(os.path.join(self.verify_dir, "sink-*.json")):
             os.unlink(f)
         for sink in self.sinks:
-            os.killpg(sink.pid, signal.SIGUSR1)
+            os.killpg(sink.pid, signal.SIGUSR2 if reset else signal.SIGUSR1)
         deadline = time.monotonic() + 60
         files = []
         while time.monotonic() < deadline:
@@ -606,6 +611,8 @@ async def rank_main(args, d: Dist) -> dict:
             await run_step(k, per_step)
         metrics.latency.reset()
         d.barrier()
+        if args.soak_minutes > 0:
+            return await run_soak(args, d, fx, svc, c, run_stream, per_step, notifiable, series, rss, scope)
         n0, s0 = c["events_received"], c["notify_delivered"]
         prof = None
         if os.environ.get("BENCH_PROFILE") and d.rank == 0:  # cProfile of the timed steps only
@@ -704,6 +711,52 @@ async def rank_main(args, d: Dist) -> dict:
                               "threads": svc.thread_placement}}
     finally:
         await fx.close()
+
+
+async def run_soak(args, d, fx, svc, c, run_stream, per_step: int, notifiable: list, series: list, rss: list,
+                   scope: str) -> dict:
+    """Saturated soak: chunks of ``--soak-chunk-steps`` steps streamed back to
+    back (the fixture sends as fast as the watcher takes them) for
+    ``--soak-minutes``. After each chunk every event is in and every
+    notification acknowledged; the sink's keys are then counted and cleared,
+    so each chunk is checked exactly-once on its own and nothing grows with
+    the run. RSS is sampled every second (the timed-steps series)."""
+    if d.rank == 0:
+        await fx.verify_counts(reset=True)  # forget the warm-up's keys
+    await d.abarrier()
+    notifiable[0] = 0
+    series.clear()
+    rss.clear()
+    chunks = []
+    k = args.warmup
+    t0 = time.perf_counter()
+    n_start = c["events_received"]
+    while time.perf_counter() - t0 < args.soak_minutes * 60:
+        n0, nb, tc = c["events_received"], notifiable[0], time.perf_counter()
+        await run_stream(k, args.soak_chunk_steps, per_step)
+        k += args.soak_chunk_steps
+        el = time.perf_counter() - tc
+        v = await fx.verify_counts(reset=True) if d.rank == 0 else None
+        await d.abarrier()  # no rank streams the next chunk before the sink is cleared
+        exp = notifiable[0] - nb
+        ch = {"t": round(time.perf_counter() - t0, 1), "seconds": round(el, 3), "events": c["events_received"] - n0,
+              "rate": round((c["events_received"] - n0) / el, 1), "rss_mib": round(_rss_mib(), 1),
+              "notify_failed": c["notify_failed"]}
+        if v is not None:
+            ch.update(expected=exp, received=v["received"], unique=v["unique"], duplicates=v["duplicates"],
+                      exactly_once=v["duplicates"] == 0 and v["unique"] == exp and v["received"] == exp)
+        chunks.append(ch)
+        print(f"soak {ch['t']:.0f}s chunk {len(chunks)}: {ch['rate']:.0f} ev/s rss {ch['rss_mib']} MiB "
+              f"exactly_once={ch.get('exactly_once')}", file=sys.stderr, flush=True)
+    elapsed = time.perf_counter() - t0
+    hub = getattr(svc, "_reader_hub", None)
+    reader = dict(hub.stats()) if hub is not None else None
+    svc.stop()
+    await svc.shutdown()
+    d.barrier()
+    return {"soak": True, "elapsed": elapsed, "events": c["events_received"] - n_start, "chunks": chunks,
+            "series": list(series), "rss_mib": list(rss), "scope": scope,
+            "reader": reader}
 
 
 async def run_latency(fx, d, svc, c, k: int, rate: float, count: int, timeout: float, notifiable: list) -> None:
@@ -852,10 +905,53 @@ def pct(samples, q: float):
     return s[max(0, min(len(s) - 1, int(-(-q * len(s) // 100)) - 1))]
 
 
+def soak_report(args, d: "Dist", res: dict) -> int:
+    elapsed = d.reduce(res["elapsed"], "MAX")
+    events = d.reduce(float(res["events"]), "SUM")
+    series = _sum_series(d.all_gather(res["series"]))
+    d.close()
+    if d.rank != 0:
+        return 0
+    chunks = res["chunks"]
+    rss = [ch["rss_mib"] for ch in chunks]  # after each chunk
+    n = len(rss)
+    slope = None
+    if n >= 10:  # least squares over the second half (after the pools have grown), MiB per hour
+        xs = [ch["t"] for ch in chunks[n // 2:]]
+        ys = rss[n // 2:]
+        mx, my = sum(xs) / len(xs), sum(ys) / len(ys)
+        den = sum((x - mx) ** 2 for x in xs)
+        slope = round(sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / den * 3600, 2) if den else None
+    out = {"metric": "saturated soak: pod-events/s sustained with per-chunk exactly-once and RSS",
+           "value": round(events / elapsed, 1), "unit": "pod-events/s", "n_gpus": d.world,
+           "minutes": round(elapsed / 60, 2), "events": int(events), "chunks": len(chunks),
+           "chunk_steps": args.soak_chunk_steps, "rounds_per_step": max(1, args.rounds_per_step),
+           "exactly_once_all": all(ch.get("exactly_once") for ch in chunks) if chunks else None,
+           "duplicates": sum(ch.get("duplicates", 0) for ch in chunks),
+           "missing": sum(ch.get("expected", 0) - ch.get("unique", 0) for ch in chunks),
+           "notify_failed": chunks[-1]["notify_failed"] if chunks else None,
+           "rate_series": _series_stats(series),
+           "chunk_rate": {"min": min(ch["rate"] for ch in chunks), "max": max(ch["rate"] for ch in chunks)}
+           if chunks else None,
+           "rss_mib": {"first": rss[0], "last": rss[-1], "max": max(rss),
+                       "slope_second_half_mib_per_hour": slope} if rss else None,
+           "config": {"profile": args.profile, "scope": res["scope"], "namespaces": args.namespaces,
+                      "pods_per_step": args.pods_per_step},
+           "reader_rank0": res["reader"], "chunk_log": chunks}
+    line = json.dumps(out)
+    print(line, flush=True)
+    if args.json_out:
+        with open(args.json_out, "w") as fh:
+            fh.write(line + "\n")
+    return 0
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     d = Dist()
     res = asyncio.run(rank_main(args, d))
+    if res.get("soak"):
+        return soak_report(args, d, res)
     elapsed = d.reduce(res["elapsed"], "MAX")
     events = d.reduce(float(res["events"]), "SUM")
     notified = d.reduce(float(res["notified"]), "SUM")

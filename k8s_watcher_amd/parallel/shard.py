@@ -27,7 +27,12 @@ Two ways to decide which shard owns what:
     or ``ceil`` of ``n / count`` namespaces. Meant for a fixed namespace
     set: when ``ceil(n / count)`` changes, a few namespaces move to another
     shard, whose first LIST re-announces their pods as ``ADDED``
-    (at-least-once across that hand-over).
+    (at-least-once for pods that exist across that hand-over). Deletions
+    are not covered: the losing shard forgets the namespace's cached pods
+    without notifying, and the gaining shard's LIST only sees pods that
+    still exist, so a pod deleted between the two shards' views of the
+    namespace set is never reported ``DELETED``. Use ``hash`` (namespaces
+    never move) where every deletion must be reported.
 
 crc32 is stable across processes and Python versions, unlike ``hash()``.
 """

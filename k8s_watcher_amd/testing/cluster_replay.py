@@ -66,8 +66,8 @@ try:  # the watcher's native module also re-stamps fixture buffers (optional her
 except Exception:  # noqa: BLE001 - fixtures must run without the extension too
     _stamp = None
 
-RV0 = 100_000_000  # every resourceVersion has exactly 9 digits
-RV_DIGITS = 9
+RV0 = 1_000_000_000  # every resourceVersion has exactly 10 digits (room for 180k steps of 50k events)
+RV_DIGITS = 10
 STEP_HEX = 8  # uid prefix: the step number
 _TYPES = (b'{"type":"ADDED","object":', b'{"type":"MODIFIED","object":', b'{"type":"MODIFIED","object":',
           b'{"type":"MODIFIED","object":', b'{"type":"DELETED","object":')

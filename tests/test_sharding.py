@@ -455,3 +455,20 @@ def test_bench_sustained_rounds_and_apart_placement():
     # every event of the timed steps is notified (the staging profile filters nothing)
     assert st["every_event_notified_per_s"] == pytest.approx(st["events_per_s"], rel=0.02)
     assert st["latency_samples"] > 0 and st["p99_latency_ms"] >= st["p50_latency_ms"] > 0
+
+
+def test_bench_saturated_soak_mode():
+    """bench.py --soak-minutes: chunks streamed back to back, each checked
+    exactly-once on its own (the sink is counted and cleared between them),
+    RSS after every chunk and its slope."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--soak-minutes", "0.08",
+                        "--soak-chunk-steps", "2", "--rounds-per-step", "2", "--pods-per-step", "300",
+                        "--namespaces", "8", "--warmup", "1", "--apart", "off", "--staging", "off",
+                        "--latency-seconds", "0", "--latency-seconds-high", "0", "--ref-events", "0",
+                        "--sink-workers", "1", "--no-placement"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["chunks"] >= 2 and d["exactly_once_all"] and d["duplicates"] == 0 and d["missing"] == 0
+    assert d["events"] == d["chunks"] * 2 * 2 * 1500 and d["value"] > 0
+    assert d["rss_mib"]["max"] >= d["rss_mib"]["first"] > 0
