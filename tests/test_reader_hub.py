@@ -421,3 +421,37 @@ def test_take_dispatch_feeds_bound_pipeline_like_handle_raw(ov):
     core.close()
     for x in (a, b, c, d):
         x.close()
+
+
+def test_buffers_grow_for_a_busy_stream_and_stay_small_for_quiet_ones():
+    """Size classes: a stream whose buffers fill before they are taken moves
+    up to buf_bytes reads; a trickling stream keeps the smallest class, so
+    many quiet streams do not starve the pool (nbufs * buf_bytes of memory)."""
+    import threading
+    mod = load()
+    core = mod.ReaderHub(1 << 20, 4)  # 4 MiB of memory: 4 big buffers, or 256 small ones
+    (a, b), (c, d) = socket.socketpair(), socket.socketpair()
+    busy, quiet = core.add(os.dup(b.fileno())), core.add(os.dup(d.fileno()))
+    payload = os.urandom(12 << 20)
+    t = threading.Thread(target=a.sendall, args=(payload,), daemon=True)
+    t.start()
+    c.sendall(b"x" * 100)
+    sizes, got, qgot = [], bytearray(), bytearray()
+    deadline = time.monotonic() + 20
+    while (len(got) < len(payload) or len(qgot) < 100) and time.monotonic() < deadline:
+        time.sleep(0.01)  # a slow consumer: buffers fill before they are taken
+        for sid, buf, view, read_ns, err in core.take():
+            if view is None:
+                continue
+            (got if sid == busy else qgot).extend(view)
+            if sid == busy:
+                sizes.append(len(view))
+            view.release()
+            core.release(buf)
+    t.join()
+    assert bytes(got) == payload and bytes(qgot) == b"x" * 100
+    assert max(sizes) > 256 << 10  # grew past the 256 KiB class
+    assert core.stats()["allocated_bytes"] <= 4 << 20
+    core.close()
+    for x in (a, b, c, d):
+        x.close()
