@@ -627,6 +627,7 @@ async def rank_main(args, d: Dist) -> dict:
         pool0 = dpool.stats() if dpool is not None else None
         gc_stats = _GcStats()  # collector pauses on the loop thread over the timed steps
         cpu0 = cpu_snapshot(fx)
+        cg0 = cgroup_cpu()
         t0 = time.perf_counter()
         if prof is not None:
             prof.enable()
@@ -644,6 +645,7 @@ async def rank_main(args, d: Dist) -> dict:
             prof.disable()
             prof.dump_stats(os.environ["BENCH_PROFILE"])
         cpu1 = cpu_snapshot(fx)
+        cg_timed = cgroup_delta(cg0, cgroup_cpu())
         pool_stats = None
         if dpool is not None:  # decode workers over the timed steps: useful lines vs idle spin/sleep
             pool1 = dpool.stats()
@@ -671,7 +673,9 @@ async def rank_main(args, d: Dist) -> dict:
             lat = list(metrics.latency.samples or [])
         # and at 10x that, long enough for >= 5,000 notified samples in the 20%-notifying profile
         lat_hi = []
+        cg_hi = None
         if args.latency_rate_high > 0 and args.latency_seconds_high > 0:
+            cg_a = cgroup_cpu()
             metrics.latency.reset()
             k_lat += 1
             count = max(1, int(args.latency_rate_high * d.world * args.latency_seconds_high))
@@ -679,6 +683,7 @@ async def rank_main(args, d: Dist) -> dict:
             await run_latency(fx, d, svc, c, k_lat, args.latency_rate_high * d.world, count, args.step_timeout,
                               notifiable)
             lat_hi = list(metrics.latency.samples or [])
+            cg_hi = cgroup_delta(cg_a, cgroup_cpu())
         failed = c["notify_failed"]
         delivered_total = c["notify_delivered"]
         hub = getattr(svc, "_reader_hub", None)
@@ -706,6 +711,7 @@ async def rank_main(args, d: Dist) -> dict:
                 "cpu_threads": sorted((round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0
                                        if k.startswith("thread_") and k != "thread_loop" and k in cpu1),
                                       reverse=True)[:8],
+                "cgroup_timed": cg_timed, "cgroup_latency_high": cg_hi,
                 "decode_threads": decode_threads, "decode_pool": pool_stats, "scope": scope, "step_phases_ms": step_phases, "probe": probe, "reader": reader,
                 "placement": {"watcher": cpu_ranges(watcher_cpus), "fixtures": cpu_ranges(fx_cpus),
                               "threads": svc.thread_placement}}
@@ -811,6 +817,36 @@ class _GcStats:
 def _rss_mib() -> float:
     with open("/proc/self/statm") as fh:
         return round(int(fh.read().split()[1]) * os.sysconf("SC_PAGE_SIZE") / 2 ** 20, 1)
+
+
+def cgroup_cpu() -> "dict | None":
+    """cgroup v2 CPU accounting of the container (cpu.stat + cpu.max): usage
+    and CFS throttling — a run that needs more than the quota in a 100 ms
+    period is stopped for the rest of it, which caps throughput and shows up
+    as multi-millisecond latency tails."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as fh:
+            st = {k: int(v) for k, v in (ln.split() for ln in fh if ln.strip())}
+    except (OSError, ValueError):
+        return None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()
+        st["quota_cpus"] = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        st["quota_cpus"] = None
+    st["t"] = time.perf_counter()
+    return st
+
+
+def cgroup_delta(a: "dict | None", b: "dict | None") -> "dict | None":
+    if not a or not b:
+        return None
+    el = max(1e-9, b["t"] - a["t"])
+    d = lambda k: b.get(k, 0) - a.get(k, 0)  # noqa: E731
+    return {"quota_cpus": b.get("quota_cpus"), "usage_cpus": round(d("usage_usec") / 1e6 / el, 2),
+            "periods": d("nr_periods"), "throttled_periods": d("nr_throttled"),
+            "throttled_ms": round(d("throttled_usec") / 1e3, 1)}
 
 
 def cpu_snapshot(fx: "Fixtures") -> dict:
@@ -1019,7 +1055,8 @@ def main(argv=None) -> int:
                    "p99_latency_ms": round(pct(lat3, 99) / 1e6, 3) if lat3 else None,
                    "exactly_once": (v3["duplicates"] == 0 and v3["unique"] == r3["notifiable"]
                                     and v3["received"] == r3["notifiable"]) if v3 else None,
-                   "delivered_by_shards": int(dl3), "cpu_util_rank0": r3["cpu_util"]}
+                   "delivered_by_shards": int(dl3), "cpu_util_rank0": r3["cpu_util"],
+                   "cgroup_timed": r3["cgroup_timed"], "cgroup_latency": r3["cgroup_latency_high"]}
     d.close()
     if d.rank != 0:
         return 0
@@ -1087,6 +1124,9 @@ def main(argv=None) -> int:
         "front_ends": res["front_ends"],
         "sink_workers": res["sink_workers"],
         "cpu_util_rank0": res["cpu_util"],
+        # the container's CPU quota and CFS throttling over the timed steps (and the high-rate latency phase)
+        "cgroup_cpu_timed": res["cgroup_timed"],
+        "cgroup_cpu_latency_high": res["cgroup_latency_high"],
         "step_phases_ms_rank0": res["step_phases_ms"],
         "step_sync": args.step_sync,
         "watch_reader_rank0": res["reader"],
