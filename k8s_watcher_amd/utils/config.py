@@ -215,7 +215,7 @@ class KubernetesSettings:
 @dataclass
 class NotifierPoolSettings:
     connections: int = 16
-    pipeline_depth: int = 8
+    pipeline_depth: int = 32
     queue_size: int = 65536
     max_queued_bytes: int = 64 << 20  # backpressure also past this many owed body bytes
     coalesce: bool = False
@@ -520,7 +520,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         retry=_retry(c.get("retry"), "clusterapi.retry", RetryPolicy(3, 2.0)),
         pool=NotifierPoolSettings(
             connections=max(1, _as_int(pool.get("connections", 16), "clusterapi.pool.connections")),
-            pipeline_depth=max(1, _as_int(pool.get("pipeline_depth", 8), "clusterapi.pool.pipeline_depth")),
+            pipeline_depth=max(1, _as_int(pool.get("pipeline_depth", 32), "clusterapi.pool.pipeline_depth")),
             queue_size=max(1, _as_int(pool.get("queue_size", 65536), "clusterapi.pool.queue_size")),
             max_queued_bytes=max(1 << 16, _as_int(pool.get("max_queued_bytes", 64 << 20),
                                                   "clusterapi.pool.max_queued_bytes")),

@@ -39,9 +39,15 @@ for step in "$@"; do
       python - "$OUT/bench_$label.json" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))
+rs = d.get("rate_series") or {}
+st = d.get("staging") or {}
 print(sys.argv[1], d["value"], "ms/step", d["ms_per_step"], "timed_s", round(d["ms_per_step"] * d["steps"] / 1e3, 2),
-      "p50", d["p50_latency_ms"], "exactly_once", (d.get("verify") or {}).get("exactly_once"),
-      "rate_series", d.get("rate_series"))
+      "p50", d["p50_latency_ms"], "hi", {k: (d.get("latency_high_rate") or {}).get(k) for k in ("p50_ms", "p99_ms")},
+      "exactly_once", (d.get("verify") or {}).get("exactly_once"),
+      "rate min/med", rs.get("min_over_median"), "notified/s", d.get("notified_per_s"),
+      "cpu", d.get("cpu_util_rank0"), "cgroup", d.get("cgroup_cpu_timed"),
+      "staging", {k: st.get(k) for k in ("every_event_notified_per_s", "p50_latency_ms", "p99_latency_ms",
+                                         "exactly_once", "cgroup_latency")} if st else None)
 PY
       ;;
     shards)
