@@ -568,10 +568,10 @@ async def rank_main(args, d: Dist) -> dict:
             t_start = time.perf_counter()
 
             async def send_all() -> int:
-                n = 0
-                for k in range(k0 * R, (k0 + steps) * R):
-                    n += int((await fx.cmd(f"STEP {k}"))[3])
-                return n
+                # one command for the whole run: the fixture's workers stream
+                # step after step without waiting on this (busy) event loop
+                # between them, so the offered load has no gaps
+                return int((await fx.cmd(f"STEPS {k0 * R} {(k0 + steps) * R}"))[3])
 
             sent = asyncio.ensure_future(send_all()) if d.rank == 0 else None
             deadline = time.monotonic() + args.step_timeout * steps

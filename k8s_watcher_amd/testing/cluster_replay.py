@@ -35,6 +35,8 @@ Control (stdin lines → one stdout line each), forwarded to every worker::
     READY {json: port, events_per_step, notifiable_per_step, namespaces}
     PREPARE <k0> <k1>          compile the open watches' scopes ahead of the first step -> OK
     STEP <k>                   stream step k to every watch       -> SENT k <events> <notifiable>
+    STEPS <k0> <k1>            steps k0..k1-1 back to back, each worker on its own (no
+                               controller round trip between steps) -> SENT k1-1 <events> <notifiable>
     PACE <k> <rate> <count>    first <count> events of step k at <rate>/s (0 = max) -> SENT k n m
     WATCHERS                   -> SENT - <open watch streams over all workers>
     QUIT
@@ -458,6 +460,9 @@ class Worker:
                 await self.prepare(int(parts[1]), int(parts[2]))
             elif cmd == "STEP":
                 await self.step(int(parts[1]))
+            elif cmd == "STEPS":  # back to back, no round trip to the controller between steps
+                for k in range(int(parts[1]), int(parts[2])):
+                    await self.step(k)
             elif cmd == "PACE":
                 await self.pace(int(parts[1]), float(parts[2]), min(int(parts[3]), self.m.E))
             elif cmd == "WATCHERS":
@@ -569,6 +574,9 @@ def run(args) -> None:
         replies = [rd.readline().decode().strip() for _, _, rd in workers]
         if cmd == "STEP":
             print(f"SENT {parts[1]} {model.E} {model.notifiable_upto(model.E)}", flush=True)
+        elif cmd == "STEPS":
+            k = int(parts[2]) - int(parts[1])
+            print(f"SENT {int(parts[2]) - 1} {model.E * k} {model.notifiable_upto(model.E) * k}", flush=True)
         elif cmd == "PACE":
             n = min(int(parts[3]), model.E)
             print(f"SENT {parts[1]} {n} {model.notifiable_upto(n)}", flush=True)
