@@ -612,7 +612,7 @@ async def rank_main(args, d: Dist) -> dict:
         metrics.latency.reset()
         d.barrier()
         if args.soak_minutes > 0:
-            return await run_soak(args, d, fx, svc, c, run_stream, per_step, notifiable, series, rss, scope)
+            return await run_soak(args, d, fx, svc, c, metrics, run_stream, per_step, notifiable, series, rss, scope)
         n0, s0 = c["events_received"], c["notify_delivered"]
         prof = None
         if os.environ.get("BENCH_PROFILE") and d.rank == 0:  # cProfile of the timed steps only
@@ -719,20 +719,22 @@ async def rank_main(args, d: Dist) -> dict:
         await fx.close()
 
 
-async def run_soak(args, d, fx, svc, c, run_stream, per_step: int, notifiable: list, series: list, rss: list,
-                   scope: str) -> dict:
+async def run_soak(args, d, fx, svc, c, metrics, run_stream, per_step: int, notifiable: list, series: list,
+                   rss: list, scope: str) -> dict:
     """Saturated soak: chunks of ``--soak-chunk-steps`` steps streamed back to
     back (the fixture sends as fast as the watcher takes them) for
     ``--soak-minutes``. After each chunk every event is in and every
     notification acknowledged; the sink's keys are then counted and cleared,
     so each chunk is checked exactly-once on its own and nothing grows with
-    the run. RSS is sampled every second (the timed-steps series)."""
+    the run. RSS is sampled after every chunk; the latency samples the bench
+    keeps are summarised (saturated p50/p99) and dropped per chunk too."""
     if d.rank == 0:
         await fx.verify_counts(reset=True)  # forget the warm-up's keys
     await d.abarrier()
     notifiable[0] = 0
     series.clear()
     rss.clear()
+    metrics.latency.reset()
     chunks = []
     k = args.warmup
     t0 = time.perf_counter()
@@ -745,9 +747,17 @@ async def run_soak(args, d, fx, svc, c, run_stream, per_step: int, notifiable: l
         v = await fx.verify_counts(reset=True) if d.rank == 0 else None
         await d.abarrier()  # no rank streams the next chunk before the sink is cleared
         exp = notifiable[0] - nb
+        sat = metrics.latency.samples
+        if sat:
+            import numpy as np
+            a = np.frombuffer(sat, dtype=np.int64)
+            p50, p99 = (float(x) for x in np.percentile(a, [50, 99], method="higher"))
         ch = {"t": round(time.perf_counter() - t0, 1), "seconds": round(el, 3), "events": c["events_received"] - n0,
               "rate": round((c["events_received"] - n0) / el, 1), "rss_mib": round(_rss_mib(), 1),
-              "notify_failed": c["notify_failed"]}
+              "notify_failed": c["notify_failed"],
+              "sat_p50_ms": round(p50 / 1e6, 3) if sat else None,
+              "sat_p99_ms": round(p99 / 1e6, 3) if sat else None}
+        metrics.latency.reset()  # the bench's raw samples would otherwise grow by 8 bytes per notification
         if v is not None:
             ch.update(expected=exp, received=v["received"], unique=v["unique"], duplicates=v["duplicates"],
                       exactly_once=v["duplicates"] == 0 and v["unique"] == exp and v["received"] == exp)
@@ -961,6 +971,9 @@ def soak_report(args, d: "Dist", res: dict) -> int:
     out = {"metric": "saturated soak: pod-events/s sustained with per-chunk exactly-once and RSS",
            "value": round(events / elapsed, 1), "unit": "pod-events/s", "n_gpus": d.world,
            "minutes": round(elapsed / 60, 2), "events": int(events), "chunks": len(chunks),
+           # excluding the pauses between chunks (sink counted and cleared)
+           "streaming_rate": round(sum(ch["events"] for ch in chunks) / max(1e-9, sum(ch["seconds"] for ch in chunks)), 1)
+           if chunks else None,
            "chunk_steps": args.soak_chunk_steps, "rounds_per_step": max(1, args.rounds_per_step),
            "exactly_once_all": all(ch.get("exactly_once") for ch in chunks) if chunks else None,
            "duplicates": sum(ch.get("duplicates", 0) for ch in chunks),
