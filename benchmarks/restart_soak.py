@@ -146,6 +146,17 @@ class Run:
                                          "--config-dir", self.cfg], cwd=ROOT, stdout=log, stderr=log,
                                         start_new_session=True)
 
+    def rss_mb(self) -> Optional[float]:
+        """Current RSS of the running watcher process (VmRSS), for the memory breakdown."""
+        try:
+            with open(f"/proc/{self.watcher.pid}/status") as fh:
+                for line in fh:
+                    if line.startswith("VmRSS:"):
+                        return int(line.split()[1]) / 1024
+        except (OSError, AttributeError):
+            pass
+        return None
+
     def kill_watcher(self) -> None:
         p = self.watcher
         peak = rss_peak_mb(p.pid)
@@ -160,9 +171,11 @@ class Run:
         while True:
             m = scrape(self.metrics_port)
             if m:
-                self.samples.append({"t": round(time.monotonic(), 3), **{k: m[k] for k in (
+                self.samples.append({"t": round(time.monotonic(), 3), "rss_mb": self.rss_mb(),
+                                     **{k: m[k] for k in (
                     "checkpoint_stall_ms", "checkpoint_write_ms", "checkpoint_bytes", "checkpoint_owed",
-                    "notify_delivered", "events_received", "cached_pods") if k in m}})
+                    "notify_delivered", "events_received", "cached_pods", "cache_bytes",
+                    "notify_outstanding_bytes", "watch_reader_allocated_bytes") if k in m}})
             if m and until(m):
                 return m
             if time.monotonic() > deadline:
@@ -209,6 +222,7 @@ class Run:
 
 
 async def amain(a) -> dict:
+    from benchmarks.soak import memory_at_peak  # soak.py imports this module
     rng = random.Random(a.seed)
     r = Run(a)
     try:
@@ -281,6 +295,9 @@ async def amain(a) -> dict:
             "checkpoints_written_last_process": m.get("checkpoints_written"),
             "owed_resent_last_process": m.get("checkpoint_owed_resent"),
             "watcher_peak_rss_mb": max(r.peaks) if r.peaks else None,
+            # the highest sampled RSS, split by the cache / owed-notification / read-buffer gauges
+            "memory_at_peak": memory_at_peak(r.samples),
+            "memory_after_initial_list": memory_at_peak([x for x in r.samples if x["t"] <= t0 + initial_s]),
             "checkpoint_interval_seconds": a.checkpoint_interval,
         }
     finally:

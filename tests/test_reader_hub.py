@@ -455,3 +455,111 @@ def test_buffers_grow_for_a_busy_stream_and_stay_small_for_quiet_ones():
     core.close()
     for x in (a, b, c, d):
         x.close()
+
+
+def test_take_dispatch_groups_many_bound_streams_like_serial_feeding():
+    """Reads of many bound streams are decoded as one batch (pl_run_group):
+    each stream's pipeline still sees exactly what serial feeding gives —
+    submits, cache, resume RV, control events — with reads of several streams
+    (and several reads of one stream) in one take."""
+    import threading
+    from test_native_pipeline import Recorder, run_native, stream
+    from k8s_watcher_amd.engine.pipeline import EventPipeline
+    from k8s_watcher_amd.metrics import Metrics
+    from k8s_watcher_amd.ops.decode import PyDecoder
+    from k8s_watcher_amd.utils.config import load_settings
+
+    data = stream()
+    want_calls, want_cache, _, want_rv, want_ctrl = run_native("production", {}, data)
+    s = load_settings("production", environ={})
+    pool = load().DecodePool(2)
+    core = load().ReaderHub(256 * 1024, 16)
+    n = 12
+    pipes, recs, socks, sids = [], [], [], []
+    for _ in range(n):
+        rec = Recorder()
+        p = EventPipeline(s, PyDecoder("production"), rec, Metrics())
+        p.log_events_setting = False
+        p.attach_native(pool)
+        p.sync_native_log()
+        a, b = socket.socketpair()
+        sid = core.add(os.dup(b.fileno()))
+        core.bind(sid, p.native, True)
+        pipes.append(p)
+        recs.append(rec)
+        socks += [a, b]
+        sids.append(sid)
+    by_sid = dict(zip(sids, pipes))
+    raw = _chunked(data, piece=3000)
+    # every stream's bytes arrive before the first take: one take holds reads of all of them
+    senders = [threading.Thread(target=socks[2 * i].sendall, args=(raw,), daemon=True) for i in range(n)]
+    for t in senders:
+        t.start()
+    time.sleep(0.2)
+    ctrl = {sid: [] for sid in sids}
+    done = []
+
+    def on_item(it):
+        sid, buf, view, read_ns, err = it
+        p = by_sid[sid]
+        if buf == -2:
+            assert not isinstance(view, BaseException), view
+            ctrl[sid].extend(e[0] for e in p.native_result(view, read_ns))
+            if err:
+                done.append(sid)
+            return
+        if view is None:
+            return
+        ctrl[sid].extend(e[0] for e in p.native_result(p.native.feed_chunked(view, read_ns), read_ns))
+        if p.native.body_done():
+            done.append(sid)
+        view.release()
+        core.release(buf)
+
+    _dispatch_until(core, lambda: len(done) == n, on_item, timeout=30)
+    for t in senders:
+        t.join()
+    assert sorted(done) == sorted(sids)
+    for sid, p, rec in zip(sids, pipes, recs):
+        assert rec.calls == want_calls
+        assert {u: list(e) for u, e in p.cache.items()} == {u: list(e) for u, e in want_cache.items()}
+        assert ctrl[sid] == want_ctrl
+        assert p.native.last_rv() == want_rv
+    for sid in sids:
+        core.unbind(sid)
+    core.close()
+    for x in socks:
+        x.close()
+
+
+def test_busy_streams_grow_only_to_their_share_of_the_pool():
+    """With many streams, a stream's buffer class stops at one buffer per
+    stream fitting the pool: 16 streams on 4 MiB read at most 256 KiB at a
+    time, so busy namespace watches do not starve each other."""
+    import threading
+    core = load().ReaderHub(1 << 20, 4)  # 4 MiB: 1 MiB, 256, 64, 16 KiB classes
+    pairs = [socket.socketpair() for _ in range(16)]
+    sids = [core.add(os.dup(b.fileno())) for _a, b in pairs]
+    busy = sids[0]
+    payload = os.urandom(8 << 20)
+    t = threading.Thread(target=pairs[0][0].sendall, args=(payload,), daemon=True)
+    t.start()
+    sizes, got = [], bytearray()
+    deadline = time.monotonic() + 20
+    while len(got) < len(payload) and time.monotonic() < deadline:
+        time.sleep(0.01)  # a slow consumer: buffers fill before they are taken
+        for sid, buf, view, read_ns, err in core.take():
+            if view is None:
+                continue
+            assert sid == busy
+            got.extend(view)
+            sizes.append(len(view))
+            view.release()
+            core.release(buf)
+    t.join()
+    assert bytes(got) == payload
+    assert 64 << 10 < max(sizes) <= 256 << 10
+    core.close()
+    for a, b in pairs:
+        a.close()
+        b.close()
