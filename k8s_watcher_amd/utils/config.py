@@ -307,6 +307,7 @@ class WatcherSettings:
     watch_reader_buffers: int = 64  # ReaderHub pool: up to this many buffers of watch_read_bytes (allocated on use)
     watch_reader_max_bytes: int = 0  # ReaderHub read-ahead over all streams (0: the whole pool)
     hub_dispatch: bool = True  # hub-read watches feed the native pipeline with no Python call per read
+    hub_framing: bool = True  # ... and the hub's thread de-chunks and splits their bodies (readerhub.inc HubFramer)
     thread_pinning: str = "auto"  # auto: loop thread on its own core when the process sits in one L3 | none
     retry: RetryPolicy = field(default_factory=lambda: RetryPolicy(3, 5.0))
     watch_timeout_seconds: int = 300
@@ -483,6 +484,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         watch_reader_buffers=max(2, _as_int(w.get("watch_reader_buffers", 64), "watcher.watch_reader_buffers")),
         watch_reader_max_bytes=max(0, _as_int(w.get("watch_reader_max_bytes", 0), "watcher.watch_reader_max_bytes")),
         hub_dispatch=_as_bool(w.get("hub_dispatch", True), "watcher.hub_dispatch"),
+        hub_framing=_as_bool(w.get("hub_framing", True), "watcher.hub_framing"),
         thread_pinning=_choice(w.get("thread_pinning", "auto"), "watcher.thread_pinning", ("auto", "none")),
         retry=_retry(w.get("retry"), "watcher.retry", RetryPolicy(3, 5.0), min_attempts=0),
         watch_timeout_seconds=_as_int(w.get("watch_timeout_seconds", 300), "watcher.watch_timeout_seconds"),

@@ -28,7 +28,8 @@ def test_auto_decode_threads():
     assert cpus.auto_decode_threads(1) == 0
     assert cpus.auto_decode_threads(2) == 0
     assert cpus.auto_decode_threads(4) == 2
-    assert cpus.auto_decode_threads(64) == 3
+    assert cpus.auto_decode_threads(5) == 3
+    assert cpus.auto_decode_threads(64) == 4
 
 
 def test_parse_cpu_list():

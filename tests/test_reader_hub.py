@@ -563,3 +563,124 @@ def test_busy_streams_grow_only_to_their_share_of_the_pool():
     for a, b in pairs:
         a.close()
         b.close()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_hub_framing_matches_pipeline_framing_on_random_chunking(seed):
+    """Once a chunked body is bound, the hub frames it (chunk de-framing and
+    line splitting on its reader thread, HubFramer) and the pipeline walks
+    line items: random chunk sizes, random send pieces and small buffers put
+    chunk headers, line ends and buffer ends everywhere — the result is
+    identical to the pipeline framing the same bytes itself."""
+    import random
+    import threading
+    from test_native_pipeline import Recorder, run_native, stream
+    from k8s_watcher_amd.engine.pipeline import EventPipeline
+    from k8s_watcher_amd.metrics import Metrics
+    from k8s_watcher_amd.ops.decode import PyDecoder
+    from k8s_watcher_amd.utils.config import load_settings
+
+    rng = random.Random(seed)
+    data = stream()
+    want_calls, want_cache, _, want_rv, want_ctrl = run_native("production", {}, data)
+    out, i = bytearray(), 0
+    while i < len(data):
+        n = rng.choice([1, 2, 7, 100, 1000, 4000, 9000, 30000])
+        part = data[i:i + n]
+        out += b"%x\r\n" % len(part) + part + b"\r\n"
+        i += n
+    raw = bytes(out + b"0\r\n\r\n")
+    s = load_settings("production", environ={})
+    rec = Recorder()
+    p = EventPipeline(s, PyDecoder("production"), rec, Metrics())
+    p.log_events_setting = False
+    p.attach_native(load().DecodePool(2))
+    p.sync_native_log()
+    core = load().ReaderHub(16 * 1024, 16)
+    a, b = socket.socketpair()
+    sid = core.add(os.dup(b.fileno()))
+    core.bind(sid, p.native, True)
+
+    def send():
+        j = 0
+        while j < len(raw):
+            n = rng.choice([1, 5, 333, 4096, 20000, 70000])
+            a.sendall(raw[j:j + n])
+            j += n
+            if rng.random() < 0.2:
+                time.sleep(0.001)
+
+    t = threading.Thread(target=send, daemon=True)
+    t.start()
+    ctrl, done = [], []
+
+    def on_item(it):
+        sid_, buf, view, read_ns, err = it
+        assert sid_ == sid and buf == -2, it  # a bound body never comes back raw
+        assert not isinstance(view, BaseException), view
+        ctrl.extend(e[0] for e in p.native_result(view, read_ns))
+        if err:
+            done.append(sid_)
+
+    _dispatch_until(core, lambda: done, on_item, timeout=30)
+    t.join()
+    assert done == [sid]
+    assert rec.calls == want_calls
+    assert {u: list(e) for u, e in p.cache.items()} == {u: list(e) for u, e in want_cache.items()}
+    assert ctrl == want_ctrl
+    assert p.native.last_rv() == want_rv and p.native.body_done()
+    assert core.stats()["framed_reads"] > 0  # the hub did frame (after the first take)
+    core.close()
+    a.close()
+    b.close()
+
+
+def test_hub_framing_reports_bad_chunk_size_like_the_pipeline():
+    """A framing error found by the hub surfaces as the pipeline's ValueError
+    for that read, after the lines before it were applied."""
+    from test_native_pipeline import Recorder, stream
+    from k8s_watcher_amd.engine.pipeline import EventPipeline
+    from k8s_watcher_amd.metrics import Metrics
+    from k8s_watcher_amd.ops.decode import PyDecoder
+    from k8s_watcher_amd.utils.config import load_settings
+
+    lines = stream().split(b"\n")
+    first, second = b"\n".join(lines[:3]) + b"\n", b"\n".join(lines[3:6]) + b"\n"
+    s = load_settings("staging", environ={})
+    rec = Recorder()
+    p = EventPipeline(s, PyDecoder("staging"), rec, Metrics())
+    p.log_events_setting = False
+    p.attach_native()
+    p.sync_native_log()
+    core = load().ReaderHub(64 * 1024, 4)
+    a, b = socket.socketpair()
+    sid = core.add(os.dup(b.fileno()))
+    core.bind(sid, p.native, True)
+    a.sendall(b"%x\r\n" % len(first) + first + b"\r\n")
+    results = []
+    deadline = time.monotonic() + 5
+    while core.stats()["reads"] < 1 and time.monotonic() < deadline:
+        time.sleep(0.01)
+    time.sleep(0.05)
+    items, _ = core.take_dispatch()  # the first read goes through the pipeline; framing is handed to the hub
+    for it in items:  # its submits (a Python notifier here)
+        p.native_result(it[2], it[3])
+    a.sendall(b"%x\r\n" % len(second) + second + b"\r\nzz\r\n")
+    _dispatch_until(core, lambda: bool(results), lambda it: results.append(it), timeout=5)
+    assert len(results) == 1
+    sid_, buf, res, _read_ns, _done = results[0]
+    assert buf == -2 and isinstance(res, ValueError) and "bad chunk size line zz" in str(res)
+    assert core.stats()["framed_reads"] > 0
+    # the lines before the error were applied (the cache has them), as when the
+    # pipeline frames the same bytes itself
+    ref = EventPipeline(s, PyDecoder("staging"), Recorder(), Metrics())
+    ref.log_events_setting = False
+    ref.attach_native()
+    with pytest.raises(ValueError, match="bad chunk size line zz"):
+        ref.native.feed_chunked(b"%x\r\n" % len(first) + first + b"\r\n" + b"%x\r\n" % len(second) + second
+                                + b"\r\nzz\r\n", 1)
+    assert {u: list(e) for u, e in p.cache.items()} == {u: list(e) for u, e in ref.cache.items()}
+    assert len(p.cache.items()) > 0
+    core.close()
+    a.close()
+    b.close()
