@@ -97,6 +97,8 @@ def test_json_invalid_is_json_loads(idx, seed, n):
     b"[1,]", b'{"a":1,}', b'{"a" 1}', b"{1:2}", b"[1 2]", b"[]", b"{}", b" [ ] ", b"[[[]]]", b"[{]}", b'"\t"',
     b"\t[]\n", b"\x0b[]", b"[1]x", b'"\\x"', b'"\\/"', b"[" * 600 + b"]" * 600, b'"\\' + b"\\" * 63 + b'"',
     b'{"a":1}{"b":2}', b'{"a":[1,{"b":null}],"c":"d"}', b"\xef\xbb\xbf{}",
+    # a close with nothing open (read below the validator's stack before round 3's fix)
+    b"]", b"}", b"]]", b"}{", b'{"a":1}}', b"[1]]", b' ] ',
 ])
 def test_json_invalid_edge_cases(data):
     assert verdicts(data) == [py_ok(data)] * 3
