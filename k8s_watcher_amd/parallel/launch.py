@@ -24,7 +24,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 def launch(shards: int, args: List[str], python: str = sys.executable) -> int:
     children: List[subprocess.Popen] = []
     for i in range(shards):
-        env = dict(os.environ, K8S_WATCHER_SHARD_INDEX=str(i), K8S_WATCHER_SHARD_COUNT=str(shards))
+        env = dict(os.environ, K8S_WATCHER_SHARD_INDEX=str(i), K8S_WATCHER_SHARD_COUNT=str(shards),
+                   K8S_WATCHER_LOCAL_PROCS=str(shards))  # they share this host's CPUs (utils/cpus.py)
         children.append(subprocess.Popen([python, os.path.join(ROOT, "main.py"), *args], env=env))
 
     stopping = False

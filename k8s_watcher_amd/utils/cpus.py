@@ -50,14 +50,32 @@ def available_cpus(root: str = "") -> int:
     return max(1, n)
 
 
+def local_processes() -> int:
+    """Watcher processes sharing this host's CPU allowance: the shard launcher
+    (parallel/launch.py) sets K8S_WATCHER_LOCAL_PROCS, torchrun LOCAL_WORLD_SIZE."""
+    for key in ("K8S_WATCHER_LOCAL_PROCS", "LOCAL_WORLD_SIZE"):
+        try:
+            n = int(os.environ.get(key, "") or 0)
+        except ValueError:
+            n = 0
+        if n > 0:
+            return n
+    return 1
+
+
 def auto_decode_threads(cpus: Optional[int] = None) -> int:
     """Extra decode workers for one watch stream: leave a CPU for the event
     loop thread and one for the notifier side, use at most 4 (the serial
     apply phase caps the gain beyond that). With the reader hub framing the
     bodies, the workers are the first on the event loop's side to touch each
     line, and a fourth one cut the loop's wait for them by ~40%
-    (profiles/hub_framing_gpu_box.md)."""
-    cpus = available_cpus() if cpus is None else cpus
+    (profiles/hub_framing_gpu_box.md).
+
+    Without an explicit count, the CPUs are this process's share of the
+    allowance when several shards run on the host: four ranks under one
+    16-CPU quota asked for ~25 CPUs with 4 workers each and were throttled in
+    123 of 134 scheduler periods (profiles/hub_framing_gpu_box.md)."""
+    cpus = available_cpus() // local_processes() if cpus is None else cpus
     return max(0, min(4, cpus - 2))
 
 

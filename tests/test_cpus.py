@@ -64,3 +64,15 @@ def test_loop_core_split(tmp_path):
     assert loop_core_split({0, 1, 8, 9}, root=str(tmp_path)) is None  # 2 cores
     write(tmp_path, "/sys/devices/system/cpu/cpu16/cache/index3/shared_cpu_list", "16-31")
     assert loop_core_split(set(range(17)), root=str(tmp_path)) is None  # spans two L3 domains
+
+
+def test_auto_decode_threads_per_local_process(monkeypatch):
+    """Shards on one host split its CPU allowance (launcher / torchrun env)."""
+    monkeypatch.setattr(cpus, "available_cpus", lambda root="": 16)
+    monkeypatch.delenv("K8S_WATCHER_LOCAL_PROCS", raising=False)
+    monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+    assert cpus.auto_decode_threads() == 4
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    assert cpus.auto_decode_threads() == 2
+    monkeypatch.setenv("K8S_WATCHER_LOCAL_PROCS", "8")
+    assert cpus.auto_decode_threads() == 0
