@@ -496,7 +496,7 @@ class WatcherService:
     def _make_decode_pool(self):
         """One decode pool for every watch scope (they share the loop thread)."""
         from ..ops.native import load
-        from ..utils.cpus import auto_decode_threads, pin_to_l3_domain
+        from ..utils.cpus import auto_decode_spin_us, auto_decode_threads, pin_to_l3_domain
         w = self.settings.watcher
         n = w.decode_threads if w.decode_threads >= 0 else auto_decode_threads()
         if n > 0 and w.decode_affinity != "none":
@@ -508,7 +508,8 @@ class WatcherService:
                                    index=w.decode_l3_domain)
             if dom:
                 self.log.info(f"Decode pool pinned to L3 domain CPUs {sorted(dom)}")
-        return load().DecodePool(n, w.decode_spin_us) if n > 0 else 0
+        spin = w.decode_spin_us if w.decode_spin_us >= 0 else auto_decode_spin_us()
+        return load().DecodePool(n, spin) if n > 0 else 0
 
     def _pin_threads(self) -> None:
         """``watcher.thread_pinning: auto``: keep one physical core of the L3

@@ -319,7 +319,7 @@ class WatcherSettings:
     decode_threads: int = -1  # native engine: extra watch-decode threads, -1 = auto (utils/cpus.py)
     decode_affinity: str = "auto"  # auto | l3 | none: keep loop thread + decode workers in one L3 domain
     decode_l3_domain: int = -1  # with affinity: index into the host's L3 domains, -1 = the current one
-    decode_spin_us: float = 0.0  # idle decode worker spins this long before it sleeps (0 = sleep at once)
+    decode_spin_us: float = -1.0  # idle decode worker spins this long before it sleeps (0 = at once, -1 = auto)
     state_format: str = "structured"  # structured | python_repr
     # native engine: payload (every raw JSON token copied into a payload passes json.loads' rules) |
     # full (each whole watch line and LIST item must: INVALID exactly when the Python engine's json.loads
@@ -496,7 +496,8 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         decode_threads=_decode_threads(w.get("decode_threads", "auto")),
         decode_affinity=_choice(w.get("decode_affinity", "auto"), "watcher.decode_affinity", ("auto", "l3", "none")),
         decode_l3_domain=_as_int(w.get("decode_l3_domain", -1), "watcher.decode_l3_domain"),
-        decode_spin_us=_bounded_float(w.get("decode_spin_us", 0), "watcher.decode_spin_us", 0.0, 1e6),
+        decode_spin_us=(-1.0 if str(w.get("decode_spin_us", "auto")).strip().lower() == "auto"
+                        else _bounded_float(w.get("decode_spin_us"), "watcher.decode_spin_us", 0.0, 1e6)),
         state_format=_choice(w.get("state_format", "structured"), "watcher.state_format", ("structured", "python_repr")),
         validate=_choice(w.get("validate", "payload"), "watcher.validate", ("off", "payload", "full")),
         event_timestamp=_choice(w.get("event_timestamp", "local"), "watcher.event_timestamp", ("local", "utc")),

@@ -79,6 +79,17 @@ def auto_decode_threads(cpus: Optional[int] = None) -> int:
     return max(0, min(4, cpus - 2))
 
 
+def auto_decode_spin_us(cpus: Optional[int] = None) -> float:
+    """Idle spin of the decode workers before they sleep: 20 us when this
+    process has CPUs to spare (a share of 8 or more), else 0. Workers still
+    hot when the next batch starts took the cluster-watch headline from
+    2.17-2.23M to 2.34M ev/s for ~0.35 CPU (profiles/decode_spin_r3_gpu_box.md);
+    under a tight shared quota that CPU is worth more to the other shards
+    (profiles/decode_spin_sink_gpu_box.md, round 2)."""
+    cpus = available_cpus() // local_processes() if cpus is None else cpus
+    return 20.0 if cpus >= 8 else 0.0
+
+
 def _parse_cpu_list(text: str) -> set:
     cpus = set()
     for part in text.strip().split(","):

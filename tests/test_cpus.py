@@ -76,3 +76,13 @@ def test_auto_decode_threads_per_local_process(monkeypatch):
     assert cpus.auto_decode_threads() == 2
     monkeypatch.setenv("K8S_WATCHER_LOCAL_PROCS", "8")
     assert cpus.auto_decode_threads() == 0
+
+
+def test_auto_decode_spin_us(monkeypatch):
+    monkeypatch.setattr(cpus, "available_cpus", lambda root="": 16)
+    monkeypatch.delenv("K8S_WATCHER_LOCAL_PROCS", raising=False)
+    monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+    assert cpus.auto_decode_spin_us() == 20.0
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    assert cpus.auto_decode_spin_us() == 0.0
+    assert cpus.auto_decode_spin_us(8) == 20.0
