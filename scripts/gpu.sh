@@ -6,6 +6,7 @@
 #   smoke                       __graft_entry__.smoke()
 #   tests                       pytest -m gpu (host tier)
 #   bench:<label>[:<args>]      bench.py, extra args comma-separated (bench:apart:--fixture-placement,apart)
+#   benchso:<label>:<so>[,<args>]  bench.py with another build of the extension (A/B of native changes)
 #   shards:<N>[:<args>]         bench.py --gpus N under torch.distributed.run (gloo barrier)
 #   storm:<label>[:<args>]      benchmarks/relist_storm.py
 #   suite                       benchmarks/suite.py (the five BASELINE configs)
@@ -50,6 +51,11 @@ print(sys.argv[1], d["value"], "ms/step", d["ms_per_step"], "timed_s", round(d["
                                          "exactly_once", "cgroup_latency")} if st else None)
 PY
       ;;
+    benchso)
+      so=${args[0]}
+      K8S_WATCHER_KWCORE_SO=$so timeout -k 10 900 python bench.py --json-out "$OUT/bench_$label.json" "${args[@]:1}" \
+        > "$OUT/bench_$label.log" 2>&1 || fail "bench $label" "$OUT/bench_$label.log"
+      python -c "import json; d=json.load(open('$OUT/bench_$label.json')); print('$label', d['value'], d['verify']['exactly_once'])" ;;
     shards)
       n=$label
       timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
