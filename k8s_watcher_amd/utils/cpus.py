@@ -63,6 +63,24 @@ def local_processes() -> int:
     return 1
 
 
+def process_cpu_share(root: str = "") -> int:
+    """CPUs this process may count on when ``local_processes()`` watchers run
+    on the host: its affinity mask when that is a subset of the host (each
+    shard pinned to its own L3 domain: those CPUs are its own), else that
+    many-th of it; and that many-th of a cgroup quota, which they all share."""
+    procs = local_processes()
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    online = os.cpu_count() or aff
+    share = aff if aff < online else aff // procs
+    limit = cgroup_cpu_limit(root)
+    if limit is not None:
+        share = min(share, math.floor(limit / procs))
+    return max(1, share)
+
+
 def auto_decode_threads(cpus: Optional[int] = None) -> int:
     """Extra decode workers for one watch stream: leave a CPU for the event
     loop thread and one for the notifier side, use at most 4 (the serial
@@ -75,7 +93,7 @@ def auto_decode_threads(cpus: Optional[int] = None) -> int:
     allowance when several shards run on the host: four ranks under one
     16-CPU quota asked for ~25 CPUs with 4 workers each and were throttled in
     123 of 134 scheduler periods (profiles/hub_framing_gpu_box.md)."""
-    cpus = available_cpus() // local_processes() if cpus is None else cpus
+    cpus = process_cpu_share() if cpus is None else cpus
     return max(0, min(4, cpus - 2))
 
 
@@ -86,7 +104,7 @@ def auto_decode_spin_us(cpus: Optional[int] = None) -> float:
     2.17-2.23M to 2.34M ev/s for ~0.35 CPU (profiles/decode_spin_r3_gpu_box.md);
     under a tight shared quota that CPU is worth more to the other shards
     (profiles/decode_spin_sink_gpu_box.md, round 2)."""
-    cpus = available_cpus() // local_processes() if cpus is None else cpus
+    cpus = process_cpu_share() if cpus is None else cpus
     return 20.0 if cpus >= 8 else 0.0
 
 

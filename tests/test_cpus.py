@@ -67,21 +67,35 @@ def test_loop_core_split(tmp_path):
 
 
 def test_auto_decode_threads_per_local_process(monkeypatch):
-    """Shards on one host split its CPU allowance (launcher / torchrun env)."""
-    monkeypatch.setattr(cpus, "available_cpus", lambda root="": 16)
+    """Shards on one host split a shared CPU allowance (launcher / torchrun
+    env): the cgroup quota always, the affinity mask only when it is the whole
+    host (a shard pinned to its own L3 domain keeps those CPUs)."""
     monkeypatch.delenv("K8S_WATCHER_LOCAL_PROCS", raising=False)
     monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+    monkeypatch.setattr(cpus.os, "cpu_count", lambda: 256)
+    # the 1-GPU box: pinned to a 16-CPU domain under a 16-CPU job quota
+    monkeypatch.setattr(cpus.os, "sched_getaffinity", lambda pid: set(range(16)))
+    monkeypatch.setattr(cpus, "cgroup_cpu_limit", lambda root="": 16.0)
     assert cpus.auto_decode_threads() == 4
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
-    assert cpus.auto_decode_threads() == 2
-    monkeypatch.setenv("K8S_WATCHER_LOCAL_PROCS", "8")
-    assert cpus.auto_decode_threads() == 0
+    assert cpus.process_cpu_share() == 4 and cpus.auto_decode_threads() == 2
+    # a whole node without a quota: a pinned shard keeps its domain
+    monkeypatch.setattr(cpus, "cgroup_cpu_limit", lambda root="": None)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert cpus.process_cpu_share() == 16 and cpus.auto_decode_threads() == 4
+    # ... an unpinned one shares the host's CPUs
+    monkeypatch.setattr(cpus.os, "sched_getaffinity", lambda pid: set(range(256)))
+    assert cpus.process_cpu_share() == 32
+    monkeypatch.setenv("K8S_WATCHER_LOCAL_PROCS", "128")
+    assert cpus.process_cpu_share() == 2 and cpus.auto_decode_threads() == 0
 
 
 def test_auto_decode_spin_us(monkeypatch):
-    monkeypatch.setattr(cpus, "available_cpus", lambda root="": 16)
     monkeypatch.delenv("K8S_WATCHER_LOCAL_PROCS", raising=False)
     monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+    monkeypatch.setattr(cpus.os, "cpu_count", lambda: 256)
+    monkeypatch.setattr(cpus.os, "sched_getaffinity", lambda pid: set(range(16)))
+    monkeypatch.setattr(cpus, "cgroup_cpu_limit", lambda root="": 16.0)
     assert cpus.auto_decode_spin_us() == 20.0
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
     assert cpus.auto_decode_spin_us() == 0.0
