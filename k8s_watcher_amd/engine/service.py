@@ -299,6 +299,8 @@ class WatcherService:
                 self.metrics.gauges["watch_reader_streams"] = lambda: float(len(hub.protos))
                 self.metrics.gauges["watch_reader_reads"] = lambda: float(hub.stats().get("reads", 0))
                 self.metrics.gauges["watch_reader_wakeups"] = lambda: float(hub.stats().get("signals", 0))
+                # reads whose chunk framing and line split ran on the reader thread (watcher.hub_framing)
+                self.metrics.gauges["watch_reader_framed_reads"] = lambda: float(hub.stats().get("framed_reads", 0))
                 # memory accounting: read buffers allocated (up to watch_reader_buffers x watch_read_bytes)
                 self.metrics.gauges["watch_reader_allocated_bytes"] = \
                     lambda: float(hub.stats().get("allocated_bytes", 0))
