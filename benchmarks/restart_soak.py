@@ -175,7 +175,8 @@ class Run:
                                      **{k: m[k] for k in (
                     "checkpoint_stall_ms", "checkpoint_write_ms", "checkpoint_bytes", "checkpoint_owed",
                     "notify_delivered", "events_received", "cached_pods", "cache_bytes",
-                    "notify_outstanding_bytes", "watch_reader_allocated_bytes") if k in m}})
+                    "notify_outstanding_bytes", "watch_reader_allocated_bytes", "malloc_in_use_bytes",
+                    "malloc_free_bytes") if k in m}})
             if m and until(m):
                 return m
             if time.monotonic() > deadline:

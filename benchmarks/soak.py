@@ -104,8 +104,13 @@ def memory_at_peak(samples: List[dict]) -> Optional[dict]:
     mib = lambda k: round((p.get(k) or 0) / 2 ** 20, 1)  # noqa: E731
     parts = {"cache": mib("cache_bytes"), "notifier_owed": mib("notify_outstanding_bytes"),
              "watch_read_buffers": mib("watch_reader_allocated_bytes")}
-    return {"t": p["t"], "rss_mb": p["rss_mb"], "accounted_mib": parts,
-            "unaccounted_mib": round(p["rss_mb"] - sum(parts.values()), 1)}
+    out = {"t": p["t"], "rss_mb": p["rss_mb"], "accounted_mib": parts,
+           "unaccounted_mib": round(p["rss_mb"] - sum(parts.values()), 1)}
+    if p.get("malloc_in_use_bytes") is not None:
+        # the C heap as glibc sees it: in use (cache, buffers and everything else
+        # malloc'd, Python's large objects included) and free but retained
+        out["c_heap_mib"] = {"in_use": mib("malloc_in_use_bytes"), "free_retained": mib("malloc_free_bytes")}
+    return out
 
 
 class Soak:
@@ -207,7 +212,7 @@ class Soak:
         s = {"t": round(time.monotonic() - self.t0, 1), "step": step, "rss_mb": v.get("VmRSS"),
              "hwm_mb": v.get("VmHWM"), "pid": self.watcher.pid}
         for k in ("cached_pods", "cache_bytes", "notify_outstanding", "notify_outstanding_bytes",
-                  "watch_reader_allocated_bytes", "watch_reader_held_bytes",
+                  "watch_reader_allocated_bytes", "watch_reader_held_bytes", "malloc_in_use_bytes", "malloc_free_bytes",
                   "checkpoint_stall_ms", "checkpoint_write_ms", "checkpoint_bytes", "events_received",
                   "notify_delivered", "expired_410", "watch_restarts", "relists", "bookmarks"):
             if k in m:

@@ -26,6 +26,7 @@
 #include <openssl/x509v3.h>
 
 #include <linux/futex.h>
+#include <malloc.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <poll.h>
@@ -2076,7 +2077,32 @@ PyObject* kw_bench_validate(PyObject*, PyObject* args) {
     return Py_BuildValue("(dn)", (double)(t1 - t0) * 1e-9, (Py_ssize_t)bad);
 }
 
+// malloc_info() -> the C heap (glibc mallinfo2, every arena): bytes in use
+// (small chunks + mmapped blocks), free inside the heap (retained, not
+// returned to the kernel), and the arenas' size. Memory accounting for the
+// watcher's RSS beyond the cache / owed notifications / read buffers.
+PyObject* kw_malloc_info(PyObject*, PyObject*) {
+    struct mallinfo2 mi = mallinfo2();
+    return Py_BuildValue("{s:n,s:n,s:n,s:n}", "in_use_bytes", (Py_ssize_t)(mi.uordblks + mi.hblkhd), "free_bytes",
+                         (Py_ssize_t)mi.fordblks, "arena_bytes", (Py_ssize_t)mi.arena, "mmap_bytes",
+                         (Py_ssize_t)mi.hblkhd);
+}
+
+// malloc_trim() -> bool: give the C heap's free pages back to the kernel
+// (every arena; the decode workers' arenas keep what their threads freed).
+// Runs without the GIL: the service calls it from an executor thread.
+PyObject* kw_malloc_trim(PyObject*, PyObject*) {
+    int r;
+    Py_BEGIN_ALLOW_THREADS
+    r = malloc_trim(0);
+    Py_END_ALLOW_THREADS
+    return PyBool_FromLong(r);
+}
+
 PyMethodDef module_methods[] = {
+    {"malloc_trim", (PyCFunction)kw_malloc_trim, METH_NOARGS, "malloc_trim() -> released (glibc malloc_trim(0), no GIL)"},
+    {"malloc_info", (PyCFunction)kw_malloc_info, METH_NOARGS,
+     "malloc_info() -> {in_use_bytes, free_bytes, arena_bytes, mmap_bytes} (glibc mallinfo2)"},
     {"json_invalid", (PyCFunction)kw_json_invalid, METH_O, "json_invalid(data) -> None | reason (json.loads semantics)"},
     {"bench_validate", (PyCFunction)kw_bench_validate, METH_VARARGS, "bench_validate(lines, repeat) -> (seconds, invalid)"},
     {"bench_parse", (PyCFunction)kw_bench_parse, METH_VARARGS, "bench_parse(data, mode=2, repeat=1)"},

@@ -328,6 +328,9 @@ class WatcherSettings:
     event_timestamp: str = "local"  # local | utc
     log_events: Optional[bool] = None  # None = follow log level (parity)
     checkpoint: CheckpointSettings = field(default_factory=CheckpointSettings)
+    # native engine: every this many seconds the C heap's free pages go back to
+    # the kernel (malloc_trim, off the event loop); 0 = never
+    malloc_trim_seconds: float = 60.0
     shard: "ShardSettings" = field(default_factory=lambda: ShardSettings())
     leader_election: LeaderElectionSettings = field(default_factory=LeaderElectionSettings)
 
@@ -485,6 +488,8 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         watch_reader_max_bytes=max(0, _as_int(w.get("watch_reader_max_bytes", 0), "watcher.watch_reader_max_bytes")),
         hub_dispatch=_as_bool(w.get("hub_dispatch", True), "watcher.hub_dispatch"),
         hub_framing=_as_bool(w.get("hub_framing", True), "watcher.hub_framing"),
+        malloc_trim_seconds=_bounded_float(w.get("malloc_trim_seconds", 60.0), "watcher.malloc_trim_seconds",
+                                           0.0, 86400.0),
         thread_pinning=_choice(w.get("thread_pinning", "auto"), "watcher.thread_pinning", ("auto", "none")),
         retry=_retry(w.get("retry"), "watcher.retry", RetryPolicy(3, 5.0), min_attempts=0),
         watch_timeout_seconds=_as_int(w.get("watch_timeout_seconds", 300), "watcher.watch_timeout_seconds"),

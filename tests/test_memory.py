@@ -1,0 +1,47 @@
+"""Memory accounting and release: the C heap gauges (glibc mallinfo2) and the
+periodic malloc_trim of the native engine (watcher.malloc_trim_seconds)."""
+
+import asyncio
+
+import pytest
+
+from k8s_watcher_amd.ops.native import load
+from k8s_watcher_amd.utils.config import ConfigError, load_settings
+
+
+def test_malloc_info_and_trim():
+    kw = load()
+    blocks = [bytearray(1 << 16) for _ in range(256)]  # 16 MiB through the C heap
+    info = kw.malloc_info()
+    assert set(info) == {"in_use_bytes", "free_bytes", "arena_bytes", "mmap_bytes"}
+    assert info["in_use_bytes"] >= 16 << 20
+    del blocks
+    assert kw.malloc_trim() in (True, False)
+    after = kw.malloc_info()
+    assert after["in_use_bytes"] < info["in_use_bytes"]
+
+
+def test_malloc_trim_setting():
+    assert load_settings("production", environ={}).watcher.malloc_trim_seconds == 60.0
+    s = load_settings("production", overrides={"watcher": {"malloc_trim_seconds": 0}}, environ={})
+    assert s.watcher.malloc_trim_seconds == 0.0
+    with pytest.raises(ConfigError):
+        load_settings("production", overrides={"watcher": {"malloc_trim_seconds": -1}}, environ={})
+
+
+def test_service_trims_periodically():
+    """The service's trim loop runs the trim off the event loop and counts it."""
+    from k8s_watcher_amd.engine.service import WatcherService
+    from k8s_watcher_amd.metrics import Metrics
+
+    class Stub:
+        metrics = Metrics()
+
+    async def body():
+        stub = Stub()
+        task = asyncio.ensure_future(WatcherService._malloc_trim_loop(stub, 0.01))
+        await asyncio.sleep(0.2)
+        task.cancel()
+        return stub.metrics.c.get("malloc_trims", 0)
+
+    assert asyncio.run(body()) >= 2
