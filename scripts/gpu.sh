@@ -58,10 +58,13 @@ PY
       python -c "import json; d=json.load(open('$OUT/bench_$label.json')); print('$label', d['value'], d['verify']['exactly_once'])" ;;
     shards)
       n=$label
+      tag=n$n
+      k=2
+      while [ -e "$OUT/bench_$tag.json" ]; do tag=n${n}_$k; k=$((k + 1)); done  # repeats of one N keep their files
       timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
-        --master-port $((29400 + n)) bench.py --gpus "$n" --ref-events 0 --json-out "$OUT/bench_n$n.json" "${args[@]}" \
-        > "$OUT/bench_n$n.log" 2>&1 || fail "shards $n" "$OUT/bench_n$n.log"
-      python -c "import json; d=json.load(open('$OUT/bench_n$n.json')); print('n$n', d['value'], d['verify']['exactly_once'], [p['elapsed'] for p in d['per_rank']])" ;;
+        --master-port $((29400 + n)) bench.py --gpus "$n" --ref-events 0 --json-out "$OUT/bench_$tag.json" "${args[@]}" \
+        > "$OUT/bench_$tag.log" 2>&1 || fail "shards $n" "$OUT/bench_$tag.log"
+      python -c "import json; d=json.load(open('$OUT/bench_$tag.json')); print('$tag', d['value'], d['verify']['exactly_once'], d.get('cgroup_cpu_timed'), [p['elapsed'] for p in d['per_rank']])" ;;
     storm)
       timeout -k 10 900 python benchmarks/relist_storm.py --json-out "$OUT/storm_$label.json" "${args[@]}" \
         > "$OUT/storm_$label.log" 2>&1 || fail "storm $label" "$OUT/storm_$label.log"
