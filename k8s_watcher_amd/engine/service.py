@@ -760,7 +760,11 @@ class WatcherService:
         loop = asyncio.get_running_loop()
         while True:
             await asyncio.sleep(period)
-            await loop.run_in_executor(None, trim)
+            try:
+                await loop.run_in_executor(None, trim)
+            except RuntimeError as exc:  # the executor is going away (shutdown)
+                self.log.debug(f"malloc_trim skipped: {exc}")
+                continue
             self.metrics.c["malloc_trims"] += 1
 
     async def _checkpoint_loop(self) -> None:
