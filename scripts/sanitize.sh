@@ -21,7 +21,7 @@ ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print
   timeout -k 10 900 python -m pytest -q -p no:cacheprovider --timeout 300 \
   tests/test_native_parity.py tests/test_native_pipeline.py tests/test_podcache.py tests/test_notifier.py \
   tests/test_spool.py tests/test_notifier_tls.py tests/test_watch_list.py tests/test_e2e_slice.py tests/test_reflector.py tests/test_http_metrics.py tests/test_reader_hub.py tests/test_reader_hub_tls.py tests/test_native_sink.py \
-  tests/test_validate.py tests/test_pyrepr.py tests/test_native_relist.py tests/test_relist_storm.py \
+  tests/test_validate.py tests/test_pyrepr.py tests/test_native_relist.py tests/test_relist_storm.py tests/test_memory.py \
   2>&1 | tee build/asan.log | tail -3
 echo "== TSan"
 K8S_WATCHER_KWCORE_SO=build/sanitize-thread/$SO \
