@@ -2,6 +2,7 @@
 periodic malloc_trim of the native engine (watcher.malloc_trim_seconds)."""
 
 import asyncio
+import os
 
 import pytest
 
@@ -14,6 +15,8 @@ def test_malloc_info_and_trim():
     blocks = [bytearray(1 << 16) for _ in range(256)]  # 16 MiB through the C heap
     info = kw.malloc_info()
     assert set(info) == {"in_use_bytes", "free_bytes", "arena_bytes", "mmap_bytes"}
+    if "asan" in os.environ.get("LD_PRELOAD", "") and info["in_use_bytes"] == 0:
+        pytest.skip("the sanitizer replaced glibc's allocator: mallinfo2 sees nothing")
     assert info["in_use_bytes"] >= 16 << 20
     del blocks
     assert kw.malloc_trim() in (True, False)
