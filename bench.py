@@ -700,7 +700,9 @@ async def rank_main(args, d: Dist) -> dict:
         if d.rank == 0:
             if args.verify:
                 verify = await fx.verify_counts()
-            if args.ref_events > 0:
+            if args.ref_events > 0 and not args.api_tls:
+                # (the reference-equivalent speaks plain http to the API server, as
+                # the reference's bench runs do: no figure against an https one)
                 ref = await run_reference(args, fx, shared, targets, k_lat + 1)
         return {"elapsed": elapsed, "events": events, "notified": notified, "series": series, "rss_mib": rss,
                 "gc": gc_report,
@@ -916,7 +918,10 @@ async def run_reference(args, fx: "Fixtures", shared: dict, targets, step: int) 
         await asyncio.sleep(0.01)
     th = threading.Thread(target=work, daemon=True)
     th.start()
-    await connected
+    while not connected.done():  # the thread may die before it connects: never wait for it then
+        if not th.is_alive():
+            raise RuntimeError("reference-equivalent pipeline ended before its watch connected")
+        await asyncio.sleep(0.01)
     for _ in range(200):
         if int((await fx.cmd("WATCHERS"))[2]) >= 1:
             break
