@@ -71,6 +71,29 @@ def test_reader_hub_on_host():
     test_reader_hub.test_take_and_remove_race_the_reader_thread()
 
 
+def test_hub_framing_and_grouped_dispatch_on_host():
+    """Round 3's reader-hub paths on the host's cores: hub-side framing against
+    the pipeline's own on random boundaries, grouped dispatch of many bound
+    streams, fair-share buffer classes; then a discover-mode bench run with
+    1,000 namespace watches, exactly-once, framed by the hub."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import test_reader_hub
+    for seed in (1, 2, 3):
+        test_reader_hub.test_hub_framing_matches_pipeline_framing_on_random_chunking(seed)
+    test_reader_hub.test_take_dispatch_groups_many_bound_streams_like_serial_feeding()
+    test_reader_hub.test_busy_streams_grow_only_to_their_share_of_the_pool()
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                          "--rounds-per-step", "1", "--apart", "off", "--staging", "off", "--ref-events", "0",
+                          "--latency-seconds", "0", "--latency-seconds-high", "0", "--watch-scope", "discover",
+                          "--namespaces", "1000"],
+                         capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["verify"]["exactly_once"] and line["per_rank"][0]["scopes"] == 1000
+    hub = line["watch_reader_rank0"]
+    assert hub["mode"] == "native" and hub["framed_reads"] > 0 and hub["hub_dispatch_watches"] == 1000
+
+
 def test_native_sink_on_host(tmp_path):
     """The bench's native stub clusterapi (_kwcore.SinkServer): pipelined answers, verify keys and
     the SO_REUSEPORT worker processes' dumps, on the host."""
