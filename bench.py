@@ -422,7 +422,13 @@ async def rank_main(args, d: Dist) -> dict:
     watcher_cpus = placement(d) if args.placement else None
     if watcher_cpus:
         os.sched_setaffinity(0, watcher_cpus)  # the decode workers inherit it
-    held = [set(x) for x in d.all_gather(sorted(watcher_cpus) if watcher_cpus else []) if x]
+    gathered = d.all_gather(sorted(watcher_cpus) if watcher_cpus else [])
+    held = [set(x) for x in gathered if x]
+    if watcher_cpus and all(r == d.rank or not (set(x) & watcher_cpus) for r, x in enumerate(gathered)):
+        # this rank's L3 domain is its own (no other rank shares it): its CPU
+        # share is that mask, not 1/N of it (utils/cpus.py process_cpu_share)
+        from k8s_watcher_amd.utils.cpus import mark_own_cpus
+        mark_own_cpus()
     fx_cpus = None
     if args.fixture_placement == "apart":
         # by default the fixtures run on the watchers' own L3 domains

@@ -20,6 +20,14 @@ and the verify-mode stub clusterapi. The schedule mixes, per step:
   from the checkpoint — nothing lost; duplicates allowed (re-sent owed
   notifications and events since the checkpoint) and counted.
 
+Every ``--census-minutes`` the watcher's ``/debug/memory`` (``metrics.debug``;
+the watcher runs with ``PYTHONTRACEMALLOC=1`` unless ``--no-tracemalloc``) is
+taken: live Python objects per type and the top tracemalloc allocation sites.
+The summary diffs the census at the end of the last process's first hour with
+its last one (``object_growth``), naming what grows outside the C heap. With
+``--out`` the summary so far is rewritten every ``--progress-minutes``
+(``"complete": false``), so a run cut short still leaves its record.
+
 Every ``--sample-seconds`` the harness records the watcher's RSS (VmRSS/VmHWM)
 and its gauges: cached pods and cache bytes, owed notifications and bytes,
 checkpoint stall. The sink's keys are handed over and reset every 50 steps
@@ -113,6 +121,39 @@ def memory_at_peak(samples: List[dict]) -> Optional[dict]:
     return out
 
 
+def object_growth(censuses: List[dict], top: int = 15) -> Optional[dict]:
+    """Census of the last process at the end of its first hour (or its first
+    one) vs its last: the Python object types and tracemalloc sites that grew."""
+    if not censuses:
+        return None
+    pid = censuses[-1]["pid"]
+    mine = [c for c in censuses if c["pid"] == pid]
+    if len(mine) < 2:
+        return None
+    first = next((c for c in mine if c["age_min"] >= 60), mine[0])
+    if first is mine[-1]:
+        first = mine[0]
+    last = mine[-1]
+    a, b = first["doc"], last["doc"]
+    types = set(a["types"]) | set(b["types"])
+    delta = sorted(((k, b["types"].get(k, 0) - a["types"].get(k, 0)) for k in types), key=lambda kv: -kv[1])
+    out = {"from": {"age_min": first["age_min"], "rss_mb": first["rss_mb"], "gc_objects": a["gc_objects"],
+                    "allocated_blocks": a["allocated_blocks"]},
+           "to": {"age_min": last["age_min"], "rss_mb": last["rss_mb"], "gc_objects": b["gc_objects"],
+                  "allocated_blocks": b["allocated_blocks"]},
+           "hours": round((last["age_min"] - first["age_min"]) / 60, 2),
+           "types_grown": [{"type": k, "delta": d} for k, d in delta[:top] if d > 0],
+           "types_shrunk": [{"type": k, "delta": d} for k, d in delta[::-1][:5] if d < 0]}
+    ta, tb = a.get("tracemalloc"), b.get("tracemalloc")
+    if ta and tb:
+        sa = {x["site"]: x["bytes"] for x in ta["top"]}
+        sb = {x["site"]: x["bytes"] for x in tb["top"]}
+        grown = sorted(((k, sb.get(k, 0) - sa.get(k, 0)) for k in set(sa) | set(sb)), key=lambda kv: -kv[1])
+        out["tracemalloc"] = {"traced_bytes_from": ta["traced_bytes"], "traced_bytes_to": tb["traced_bytes"],
+                              "sites_grown": [{"site": k, "bytes": d} for k, d in grown[:top] if d > 0]}
+    return out
+
+
 class Soak:
     def __init__(self, a) -> None:
         self.a = a
@@ -128,6 +169,8 @@ class Soak:
         self.kinds: Dict[int, str] = {}
         self.kills = 0
         self.t0 = time.monotonic()
+        self.censuses: List[dict] = []
+        self.watcher_started = self.t0
 
     # ------------------------------------------------------------------ fixtures
     async def start(self) -> None:
@@ -171,7 +214,7 @@ class Soak:
                 clusterapi:
                   health_check_on_start: false
                   retry: {{max_attempts: 10, delay_seconds: 0.2}}
-                metrics: {{enabled: true, host: 127.0.0.1, port: {self.metrics_port}}}
+                metrics: {{enabled: true, host: 127.0.0.1, port: {self.metrics_port}, debug: true}}
                 watcher:
                   retry: {{max_attempts: 0, delay_seconds: 0.1, max_delay_seconds: 2}}
                   checkpoint: {{path: {os.path.join(self.dir, "state", "checkpoint.bin")}, interval_seconds: 5}}
@@ -194,9 +237,27 @@ class Soak:
 
     def start_watcher(self) -> None:
         log = open(os.path.join(self.dir, "watcher.log"), "ab")
+        env = dict(os.environ)
+        if self.a.tracemalloc:
+            env["PYTHONTRACEMALLOC"] = "1"  # one frame per allocation site: /debug/memory's top sites
         self.watcher = subprocess.Popen([sys.executable, os.path.join(ROOT, "main.py"), "production",
                                          "--config-dir", self.cfg], cwd=ROOT, stdout=log, stderr=log,
-                                        start_new_session=True)
+                                        start_new_session=True, env=env)
+        self.watcher_started = time.monotonic()
+
+    def census(self) -> None:
+        """The watcher's Python object census (``/debug/memory``)."""
+        import urllib.request
+        try:
+            with urllib.request.urlopen(f"http://127.0.0.1:{self.metrics_port}/debug/memory", timeout=30) as r:
+                doc = json.loads(r.read())
+        except (OSError, ValueError) as exc:
+            print(f"census failed: {exc}", file=sys.stderr, flush=True)
+            return
+        v = vm(self.watcher.pid)
+        self.censuses.append({"t": round(time.monotonic() - self.t0, 1), "pid": self.watcher.pid,
+                              "age_min": round((time.monotonic() - self.watcher_started) / 60, 1),
+                              "rss_mb": v.get("VmRSS"), "doc": doc})
 
     async def wait_watching(self) -> None:
         for _ in range(6000):
@@ -292,7 +353,16 @@ async def amain(a) -> dict:
         last_sample = 0.0
         next_harvest = 50
         events = s.E
+        next_census = time.monotonic() + 60.0  # one early census, then every --census-minutes
+        next_progress = time.monotonic() + a.progress_minutes * 60
         while time.monotonic() < end:
+            if time.monotonic() >= next_census:
+                s.census()
+                next_census = time.monotonic() + a.census_minutes * 60
+            if a.out and time.monotonic() >= next_progress:
+                write_out(a.out, {"summary": summarize(s, a, step, events, complete=False),
+                                  "samples": s.samples, "verdicts": s.verdicts, "censuses": s.censuses})
+                next_progress = time.monotonic() + a.progress_minutes * 60
             t_step = time.monotonic()
             half = s.E // 2
             in_kill_window = a.kill_window_minutes is None or time.monotonic() - s.t0 < a.kill_window_minutes * 60
@@ -339,31 +409,46 @@ async def amain(a) -> dict:
         # let the stream finish, then judge everything
         await asyncio.sleep(max(5.0, a.step_seconds))
         s.sample(step)
+        s.census()
         s.harvest(step + 1)
-        after = [x for x in s.samples if x["t"] >= a.warmup_minutes * 60 and x.get("rss_mb")]
-        bad = [v for v in s.verdicts if not v["ok"]]
-        last = s.samples[-1]
-        summary = {
-            "minutes": a.minutes, "steps": step, "events_replayed": events, "pods_per_step": a.pods,
-            "watcher_kills": s.kills,
-            "steps_by_kind": {k: sum(1 for v in s.verdicts if v["kind"] == k)
-                              for k in ("normal", "drop", "expire", "kill", "pre-kill")},
-            "steps_failed": len(bad), "failed_examples": bad[:5],
-            "duplicates_outside_kill_steps": sum(v["duplicates"] for v in s.verdicts
-                                                 if v["kind"] not in ("kill", "pre-kill")),
-            "duplicates_in_kill_steps": sum(v["duplicates"] for v in s.verdicts if v["kind"] in ("kill", "pre-kill")),
-            "notifications_checked": sum(v["received"] for v in s.verdicts),
-            "rss_mb_after_warmup": {"min": min(x["rss_mb"] for x in after) if after else None,
-                                    "max": max(x["rss_mb"] for x in after) if after else None,
-                                    "slope_mib_per_hour": slope_mib_per_hour([(x["t"], x["rss_mb"]) for x in after])},
-            "peak_rss_mb_last_process": last.get("hwm_mb"),
-            "rss_segments": rss_segments(s.samples, a.warmup_minutes),
-            "memory_at_peak": memory_at_peak(s.samples),
-            "last_sample": last,
-        }
-        return {"summary": summary, "samples": s.samples, "verdicts": s.verdicts}
+        return {"summary": summarize(s, a, step, events, complete=True), "samples": s.samples,
+                "verdicts": s.verdicts, "censuses": s.censuses}
     finally:
         await s.close()
+
+
+def write_out(path: str, doc: dict) -> None:
+    tmp = path + ".tmp"
+    with open(tmp, "w") as fh:
+        json.dump(doc, fh, indent=1)
+    os.replace(tmp, path)
+
+
+def summarize(s: "Soak", a, step: int, events: int, complete: bool) -> dict:
+    after = [x for x in s.samples if x["t"] >= a.warmup_minutes * 60 and x.get("rss_mb")]
+    bad = [v for v in s.verdicts if not v["ok"]]
+    last = s.samples[-1] if s.samples else {}
+    summary = {
+        "complete": complete, "elapsed_minutes": round((time.monotonic() - s.t0) / 60, 1),
+        "minutes": a.minutes, "steps": step, "events_replayed": events, "pods_per_step": a.pods,
+        "watcher_kills": s.kills,
+        "steps_by_kind": {k: sum(1 for v in s.verdicts if v["kind"] == k)
+                          for k in ("normal", "drop", "expire", "kill", "pre-kill")},
+        "steps_failed": len(bad), "failed_examples": bad[:5],
+        "duplicates_outside_kill_steps": sum(v["duplicates"] for v in s.verdicts
+                                             if v["kind"] not in ("kill", "pre-kill")),
+        "duplicates_in_kill_steps": sum(v["duplicates"] for v in s.verdicts if v["kind"] in ("kill", "pre-kill")),
+        "notifications_checked": sum(v["received"] for v in s.verdicts),
+        "rss_mb_after_warmup": {"min": min(x["rss_mb"] for x in after) if after else None,
+                                "max": max(x["rss_mb"] for x in after) if after else None,
+                                "slope_mib_per_hour": slope_mib_per_hour([(x["t"], x["rss_mb"]) for x in after])},
+        "peak_rss_mb_last_process": last.get("hwm_mb"),
+        "rss_segments": rss_segments(s.samples, a.warmup_minutes),
+        "memory_at_peak": memory_at_peak(s.samples),
+        "object_growth": object_growth(s.censuses),
+        "last_sample": last,
+    }
+    return summary
 
 
 def main(argv=None) -> int:
@@ -377,13 +462,18 @@ def main(argv=None) -> int:
     ap.add_argument("--sample-seconds", type=float, default=10.0)
     ap.add_argument("--warmup-minutes", type=float, default=5.0)
     ap.add_argument("--sink-workers", type=int, default=2)
+    ap.add_argument("--census-minutes", type=float, default=60.0,
+                    help="take the watcher's /debug/memory object census this often (and once at minute 1)")
+    ap.add_argument("--no-tracemalloc", dest="tracemalloc", action="store_false",
+                    help="run the watcher without PYTHONTRACEMALLOC (object counts only)")
+    ap.add_argument("--progress-minutes", type=float, default=15.0,
+                    help="with --out: rewrite the summary so far this often")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     res = asyncio.run(amain(a))
     print(json.dumps(res["summary"], indent=1))
     if a.out:
-        with open(a.out, "w") as fh:
-            json.dump(res, fh, indent=1)
+        write_out(a.out, res)
     return 0 if res["summary"]["steps_failed"] == 0 else 1
 
 

@@ -357,7 +357,7 @@ class LeaderElectedService:
         if self.settings.metrics.enabled:  # one server for every term, standby included
             from ..metrics import start_metrics_server
             metrics_server = await start_metrics_server(self.metrics, self.settings.metrics.host,
-                                                        self.settings.metrics.port)
+                                                        self.settings.metrics.port, debug=self.settings.metrics.debug)
         self.elector = LeaderElector(api, shard_lease(self.settings), self.metrics)
         elector_task = asyncio.ensure_future(self.elector.run())
         stopper = asyncio.ensure_future(self._stop.wait())

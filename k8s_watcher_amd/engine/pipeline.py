@@ -137,6 +137,17 @@ class EventPipeline:
         self.notifier.flush()
         self.elog.flush()
 
+    def shared_flush(self):
+        """The part of :meth:`flush_outputs` every scope sharing this notifier
+        and event log has in common — a closure over those two only, so the
+        reader hub's per-notifier flush keeps no scope's pipeline alive."""
+        notifier, elog = self.notifier, self.elog
+
+        def flush() -> None:
+            notifier.flush()
+            elog.flush()
+        return flush
+
     def sync_native_log(self) -> None:
         """Hand the event-log switches (log_events, DEBUG on) to the native side."""
         log_events = self.log_events

@@ -417,8 +417,9 @@ class Reflector:
         self.watch_count += 1
         self.connected.set()
         if (native is not None and framed[0] and w.hub_dispatch
-                and self.stream.bind_native(native, on_native, pipeline.flush_outputs,
-                                            (id(pipeline.notifier), id(pipeline.elog)))):
+                and self.stream.bind_native(native, on_native, pipeline.shared_flush(),
+                                            (id(pipeline.notifier), id(pipeline.elog)),
+                                            sync=pipeline.sync_native_log)):
             self._rv_native = native.last_rv
             pipeline.sync_native_log()
             self.metrics.c["watches_hub_dispatch"] += 1

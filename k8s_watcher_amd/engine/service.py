@@ -306,6 +306,12 @@ class WatcherService:
                     lambda: float(hub.stats().get("allocated_bytes", 0))
                 self.metrics.gauges["watch_reader_held_bytes"] = lambda: float(hub.stats().get("held_bytes", 0))
             self._pin_threads()
+        if owed:
+            # the checkpoint's cut: clusterapi never acknowledged these; send them
+            # (in their original order) before anything newer — the watches that
+            # resume after them, and the DELETEDs synthesized just below, which
+            # must be the last word for their pods
+            self._resubmit_owed(owed)
         if saved_rvs and None not in scopes:
             if self.ns_watcher is not None:
                 # namespaces deleted while the watcher was down: their pods get
@@ -314,10 +320,6 @@ class WatcherService:
                 self._notify_deleted_namespaces(set(self.ns_watcher.names))
             # pods of namespaces this shard no longer watches would never be reconciled
             self._forget_namespaces_except(set(scopes))
-        if owed:
-            # the checkpoint's cut: clusterapi never acknowledged these; send them
-            # (in their original order) before the watches resume after them
-            self._resubmit_owed(owed)
         self.metrics.gauges["cached_pods"] = lambda: float(len(cache))
         if hasattr(cache, "memory"):  # native cache: bytes held (cores + keys), for memory accounting
             self.metrics.gauges["cache_bytes"] = lambda: float(sum(v for k, v in cache.memory().items()
@@ -339,7 +341,8 @@ class WatcherService:
         for ns in scopes:
             self._start_scope(ns, primed=bool(saved_rvs))
         if s.metrics.enabled and self.serve_metrics:
-            self._metrics_server = await start_metrics_server(self.metrics, s.metrics.host, s.metrics.port)
+            self._metrics_server = await start_metrics_server(self.metrics, s.metrics.host, s.metrics.port,
+                                                              debug=s.metrics.debug)
         if ck:
             self._tasks.append(asyncio.ensure_future(self._checkpoint_loop()))
         if self._native_pipeline() and s.watcher.malloc_trim_seconds > 0:
@@ -649,6 +652,11 @@ class WatcherService:
                 self.api.http.reader_hub = None
             self._reader_hub.close()
             self._reader_hub = None
+        if self._decode_pool:
+            # its threads end now, not when the garbage collector frees this
+            # service (a leader's every term builds a new one; the shared
+            # Metrics gauges keep the old one reachable until the next term)
+            self._decode_pool.close()
         if self._loop_affinity is not None:
             try:
                 os.sched_setaffinity(0, self._loop_affinity)

@@ -13,7 +13,7 @@ from __future__ import annotations
 import json
 from typing import Callable, Dict, Optional, Tuple
 
-from ..net.http import HttpClient, HttpError, Response, StreamResponse, parse_retry_after  # noqa: F401
+from ..net.http import HttpClient, HttpError, Response, StreamResponse, json_input, parse_retry_after  # noqa: F401
 from .kubeconfig import KubeEndpoint
 
 USER_AGENT = "k8s-watcher-amd/1.0"
@@ -32,7 +32,7 @@ class ApiError(Exception):
         self.retry_after = parse_retry_after((headers or {}).get("retry-after"))
         msg = reason
         try:
-            doc = json.loads(body)
+            doc = json.loads(json_input(body))
             msg = doc.get("message") or reason
             self.k8s_reason = doc.get("reason")
         except (ValueError, AttributeError):
@@ -203,7 +203,7 @@ def lease_path(namespace: str, name: Optional[str] = None) -> str:
 
 def split_list_body(body: bytes) -> Tuple[Dict, list]:
     """Parse a ``*List`` body into ``(metadata, items)`` with the stdlib decoder."""
-    doc = json.loads(body)
+    doc = json.loads(json_input(body))
     return doc.get("metadata") or {}, doc.get("items") or []
 
 

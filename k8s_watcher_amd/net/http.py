@@ -59,8 +59,14 @@ class Response:
 
     def json(self):
         import json
-        body = self.body
-        return json.loads(body if isinstance(body, (bytes, bytearray)) else bytes(body))
+        return json.loads(json_input(self.body))
+
+
+def json_input(body):
+    """``body`` as something ``json.loads`` takes: a large body is an anonymous
+    mapping (:func:`_body_buffer`), which it does not (only str, bytes and
+    bytearray). The copy happens only for those bodies."""
+    return body if isinstance(body, (bytes, bytearray, str)) else bytes(body)
 
 
 def _body_buffer(n: int):
@@ -414,6 +420,7 @@ class _ClientProtocol(asyncio.BufferedProtocol):
         self.hub = None  # net/reader.WatchReaderHub that reads this socket, once adopted
         self.hub_sid = 0
         self.hub_result: Optional[Callable[[tuple, int, bool], None]] = None  # bind_native
+        self.hub_sync: Optional[Callable[[], None]] = None  # bind_native: the bound pipeline's log switches
 
     def deliver(self, data: bytes) -> None:
         """``parser.on_body`` for streams: body bytes + the socket-read timestamp."""
@@ -596,7 +603,7 @@ class StreamResponse:
     def last_activity(self) -> float:
         return self._proto.last_activity
 
-    def bind_native(self, pipeline_core, on_result, flush, flush_key) -> bool:
+    def bind_native(self, pipeline_core, on_result, flush, flush_key, sync=None) -> bool:
         """A hub-read watch body (net/reader.py) goes straight from the hub's
         buffers into the fused native ``pipeline_core`` — no Python call per
         socket read; ``on_result(result, read_ns, body_done)`` gets only the
@@ -608,12 +615,13 @@ class StreamResponse:
         if (hub is None or parser.state != ResponseParser.RAW or parser.buf or p.stream_sink is None
                 or p.closed.done()):
             return False
-        hub.bind(p, pipeline_core, parser.raw_chunked, on_result, flush, flush_key)
+        hub.bind(p, pipeline_core, parser.raw_chunked, on_result, flush, flush_key, sync)
         return p.hub_result is not None
 
     def close(self) -> None:
         self._proto.stream_sink = None
         self._proto.hub_result = None
+        self._proto.hub_sync = None
         self._proto.close()
 
 

@@ -86,18 +86,22 @@ class WatchReaderHub:
     def error_text(self, sid: int) -> str:
         return "" if self.closed else self.core.error_text(sid)
 
-    def bind(self, proto, pipeline_core, framed: bool, on_result, flush, flush_key) -> None:
+    def bind(self, proto, pipeline_core, framed: bool, on_result, flush, flush_key, sync=None) -> None:
         """Feed ``proto``'s body straight to a fused ``_kwcore.Pipeline`` on
         the hub's dispatch (no Python call per read): only reads whose result
         needs Python — control events, log lines, submissions, the end of the
         body, an error — come back, through ``on_result(result, read_ns,
         body_done)``. ``flush`` runs once per dispatch that fed a bound stream
         (one per distinct ``flush_key``: streams sharing a notifier flush it
-        once)."""
+        once; it should hold only what they share, so a retired stream's
+        pipeline is not kept alive by it). ``sync`` is this stream's own
+        per-dispatch hook (its pipeline's log switches): it runs after every
+        dispatch that touched the stream, and goes away with the stream."""
         if self.closed or proto.hub is not self:
             return
         self.core.bind(proto.hub_sid, pipeline_core, framed)
         proto.hub_result = on_result
+        proto.hub_sync = sync
         self._flush[flush_key] = flush
 
     def forget(self, sid: int) -> None:
@@ -122,6 +126,11 @@ class WatchReaderHub:
             self._deliver(core, items)
         finally:
             if touched:
+                for sid in touched:
+                    proto = protos.get(sid)
+                    sync = getattr(proto, "hub_sync", None) if proto is not None else None
+                    if sync is not None:
+                        sync()
                 for flush in list(self._flush.values()):
                     flush()
 

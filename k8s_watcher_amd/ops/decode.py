@@ -26,6 +26,7 @@ import json
 from typing import Any, Dict, List, Optional, Tuple
 
 from ..models.payload import build_core
+from ..net.http import json_input
 
 E_TYPE, E_UID, E_NS, E_NAME, E_RV, E_PHASE, E_HAS_STATUS, E_OBJ, E_EXTRA = range(9)
 
@@ -139,7 +140,7 @@ class PyDecoder:
         return event_from_object(etype, obj)
 
     def decode_list(self, body: bytes) -> Tuple[Optional[str], Optional[str], List[tuple]]:
-        doc = json.loads(body)
+        doc = json.loads(json_input(body))  # a LIST page over 4 MiB arrives as an mmap
         md = doc.get("metadata") or {}
         items = doc.get("items") or []
         return (md.get("resourceVersion"), md.get("continue") or None,

@@ -270,6 +270,7 @@ class MetricsSettings:
     enabled: bool = False
     host: str = "0.0.0.0"
     port: int = 9090
+    debug: bool = False  # also serve /debug/memory (Python object census, tracemalloc top sites)
 
 
 @dataclass
@@ -559,6 +560,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         enabled=_as_bool(m.get("enabled", False), "metrics.enabled"),
         host=str(m.get("host", "0.0.0.0")),
         port=_as_int(m.get("port", 9090), "metrics.port"),
+        debug=_as_bool(m.get("debug", False), "metrics.debug"),
     )
     return Settings(environment, kube, watcher, clusterapi, metrics, cfg)
 

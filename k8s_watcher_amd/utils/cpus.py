@@ -63,18 +63,31 @@ def local_processes() -> int:
     return 1
 
 
+OWN_CPUS_ENV = "K8S_WATCHER_OWN_CPUS"
+
+
+def mark_own_cpus() -> None:
+    """Declare this process's affinity mask its own: whoever set it (the
+    benchmark's per-rank L3 placement, a launcher pinning each shard) gave
+    the other local shards disjoint masks. Threads and children started
+    later see it through the environment."""
+    os.environ[OWN_CPUS_ENV] = "1"
+
+
 def process_cpu_share(root: str = "") -> int:
     """CPUs this process may count on when ``local_processes()`` watchers run
-    on the host: its affinity mask when that is a subset of the host (each
-    shard pinned to its own L3 domain: those CPUs are its own), else that
-    many-th of it; and that many-th of a cgroup quota, which they all share."""
+    on the host: that many-th of its affinity mask — a cpuset container
+    (``--cpuset-cpus``, a Kubernetes static CPU policy) gives every shard in it
+    the same mask — unless the mask was declared this shard's own
+    (:func:`mark_own_cpus`: each shard pinned to its own L3 domain); and that
+    many-th of a cgroup quota, which they all share."""
     procs = local_processes()
     try:
         aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         aff = os.cpu_count() or 1
-    online = os.cpu_count() or aff
-    share = aff if aff < online else aff // procs
+    own = os.environ.get(OWN_CPUS_ENV, "") not in ("", "0")
+    share = aff if own else aff // procs
     limit = cgroup_cpu_limit(root)
     if limit is not None:
         share = min(share, math.floor(limit / procs))

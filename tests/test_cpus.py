@@ -2,6 +2,8 @@
 
 import os
 
+import pytest
+
 from k8s_watcher_amd.utils import cpus
 
 
@@ -72,6 +74,7 @@ def test_auto_decode_threads_per_local_process(monkeypatch):
     host (a shard pinned to its own L3 domain keeps those CPUs)."""
     monkeypatch.delenv("K8S_WATCHER_LOCAL_PROCS", raising=False)
     monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+    monkeypatch.delenv(cpus.OWN_CPUS_ENV, raising=False)
     monkeypatch.setattr(cpus.os, "cpu_count", lambda: 256)
     # the 1-GPU box: pinned to a 16-CPU domain under a 16-CPU job quota
     monkeypatch.setattr(cpus.os, "sched_getaffinity", lambda pid: set(range(16)))
@@ -79,10 +82,12 @@ def test_auto_decode_threads_per_local_process(monkeypatch):
     assert cpus.auto_decode_threads() == 4
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
     assert cpus.process_cpu_share() == 4 and cpus.auto_decode_threads() == 2
-    # a whole node without a quota: a pinned shard keeps its domain
+    # a whole node without a quota: a shard pinned to its own domain keeps it
     monkeypatch.setattr(cpus, "cgroup_cpu_limit", lambda root="": None)
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    monkeypatch.setenv(cpus.OWN_CPUS_ENV, "1")
     assert cpus.process_cpu_share() == 16 and cpus.auto_decode_threads() == 4
+    monkeypatch.delenv(cpus.OWN_CPUS_ENV)
     # ... an unpinned one shares the host's CPUs
     monkeypatch.setattr(cpus.os, "sched_getaffinity", lambda pid: set(range(256)))
     assert cpus.process_cpu_share() == 32
@@ -100,3 +105,55 @@ def test_auto_decode_spin_us(monkeypatch):
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
     assert cpus.auto_decode_spin_us() == 0.0
     assert cpus.auto_decode_spin_us(8) == 20.0
+
+
+def test_cpuset_container_splits_the_mask_between_local_shards(monkeypatch):
+    """A cpuset-limited container (mask smaller than the host, no CFS quota)
+    running N shards: every shard sees the same mask, so each gets 1/N of it —
+    not the whole mask (advisor round 3: 4 workers and a 20 us spin each)."""
+    monkeypatch.delenv("K8S_WATCHER_LOCAL_PROCS", raising=False)
+    monkeypatch.delenv(cpus.OWN_CPUS_ENV, raising=False)
+    monkeypatch.setattr(cpus.os, "cpu_count", lambda: 256)
+    monkeypatch.setattr(cpus.os, "sched_getaffinity", lambda pid: set(range(16)))
+    monkeypatch.setattr(cpus, "cgroup_cpu_limit", lambda root="": None)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    assert cpus.process_cpu_share() == 4
+    assert cpus.auto_decode_threads() == 2 and cpus.auto_decode_spin_us() == 0.0
+    monkeypatch.setenv(cpus.OWN_CPUS_ENV, "1")  # the launcher pinned each shard to its own 16
+    assert cpus.process_cpu_share() == 16 and cpus.auto_decode_spin_us() == 20.0
+
+
+@pytest.mark.parametrize("own", [False, True])
+def test_eight_local_ranks_get_sane_shares(monkeypatch, own):
+    """The driver's 8-GPU node runs bench.py with 8 local ranks. Whatever
+    the node looks like, no rank may plan for more CPUs than its share, and
+    the ranks together never plan more decode workers + loop threads than
+    the CPUs they have."""
+    monkeypatch.delenv("K8S_WATCHER_LOCAL_PROCS", raising=False)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    if own:
+        monkeypatch.setenv(cpus.OWN_CPUS_ENV, "1")
+    else:
+        monkeypatch.delenv(cpus.OWN_CPUS_ENV, raising=False)
+    monkeypatch.setattr(cpus.os, "cpu_count", lambda: 256)
+    shapes = [  # (mask, quota)
+        (set(range(256)), None),    # whole node
+        (set(range(128)), 128.0),   # half the node, quota to match
+        (set(range(64)), 32.0),     # cpuset + tighter quota
+        (set(range(16)), 16.0),     # the 1-GPU box's allowance
+        (set(range(8)), None),      # a small cpuset
+    ]
+    for mask, quota in shapes:
+        if own:  # placement: each rank pinned to a disjoint 1/8 of the mask
+            mine = set(sorted(mask)[:max(1, len(mask) // 8)])
+        else:
+            mine = mask
+        monkeypatch.setattr(cpus.os, "sched_getaffinity", lambda pid, m=mine: set(m))
+        monkeypatch.setattr(cpus, "cgroup_cpu_limit", lambda root="", q=quota: q)
+        share = cpus.process_cpu_share()
+        total = quota if quota is not None else len(mask)
+        assert 1 <= share <= max(1, total // 8), (mask, quota, share)
+        workers = cpus.auto_decode_threads()
+        assert 8 * (workers + 1) <= max(8, total), (mask, quota, workers)
+        # spinning only with CPUs to spare
+        assert cpus.auto_decode_spin_us() == (20.0 if share >= 8 else 0.0)

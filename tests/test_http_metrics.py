@@ -150,3 +150,28 @@ def test_closed_streams_leave_the_client():
     got, left, bufs = run(body())
     assert len(got) == 5 and left == 0
     assert all(b is None for b in bufs)
+
+def test_debug_memory_endpoint_only_when_enabled():
+    import tracemalloc
+
+    async def body():
+        m = Metrics()
+        plain = await start_metrics_server(m, "127.0.0.1", 0)
+        dbg = await start_metrics_server(m, "127.0.0.1", 0, debug=True)
+        out = []
+        for srv in (plain, dbg):
+            c = HttpClient(f"http://127.0.0.1:{srv.sockets[0].getsockname()[1]}")
+            r = await c.request("GET", "/debug/memory")
+            out.append((r.status, r.json() if r.status == 200 else None))
+            await c.close()
+            srv.close()
+        return out
+
+    tracemalloc.start()
+    try:
+        (s0, _), (s1, doc) = run(body())
+    finally:
+        tracemalloc.stop()
+    assert s0 == 404 and s1 == 200
+    assert doc["gc_objects"] > 1000 and "builtins.dict" in doc["types"]
+    assert doc["tracemalloc"]["traced_bytes"] > 0 and doc["tracemalloc"]["top"]

@@ -684,3 +684,60 @@ def test_hub_framing_reports_bad_chunk_size_like_the_pipeline():
     core.close()
     a.close()
     b.close()
+
+
+def test_runtime_log_level_reaches_every_hub_dispatched_scope():
+    """Several namespace scopes share one notifier and event log, so the hub
+    flushes them once per dispatch; each bound scope's native pipeline must
+    still pick up a runtime change of the log switches (advisor round 3: only
+    the last-bound scope's pipeline did)."""
+    import logging
+
+    from conftest import run
+    from k8s_watcher_amd.engine.service import WatcherService
+    from k8s_watcher_amd.kube.kubeconfig import KubeEndpoint
+    from k8s_watcher_amd.metrics import Metrics
+    from k8s_watcher_amd.testing.fake_apiserver import FakeApiServer
+    from k8s_watcher_amd.testing.podgen import PodFactory
+    from k8s_watcher_amd.testing.stub_sink import StubSink
+    from k8s_watcher_amd.utils.config import load_settings
+    from k8s_watcher_amd.utils.logsetup import SERVICE_LOGGER
+
+    names = ["ns-a", "ns-b", "ns-c"]
+
+    async def body():
+        srv = FakeApiServer(namespaces=names)
+        await srv.start()
+        sink = StubSink()
+        await sink.start()
+        s = load_settings("staging", overrides={
+            "clusterapi": {"base_url": sink.url, "health_check_on_start": False},
+            "watcher": {"engine": "native", "namespace_scope": "discover", "watch_reader": "native",
+                        "hub_dispatch": True, "retry": {"delay_seconds": 0.05, "max_attempts": 0}}})
+        log = logging.getLogger(SERVICE_LOGGER)
+        old = log.level
+        log.setLevel(logging.WARNING)
+        svc = WatcherService(s, endpoint=KubeEndpoint(server=srv.url), metrics=Metrics())
+        try:
+            await svc.start()
+            f = PodFactory(seed=3, namespaces=names)
+            for ns in names:
+                srv.create(f.new_pod(namespace=ns))
+            await sink.state.wait_for(3, timeout=10)
+            assert svc.metrics.c["watches_hub_dispatch"] == len(names)
+            assert {r.pipeline._native_log for r in svc.reflectors} == {(False, False)}
+            log.setLevel(logging.INFO)  # at run time: every scope's native pipeline must follow
+            for ns in names:
+                srv.create(f.new_pod(namespace=ns))
+            await sink.state.wait_for(6, timeout=10)
+            flags = sorted((r.namespace, r.pipeline._native_log) for r in svc.reflectors)
+        finally:
+            log.setLevel(old)
+            svc.stop()
+            await svc.shutdown()
+            await sink.stop()
+            await srv.stop()
+        return flags
+
+    flags = run(body(), timeout=60)
+    assert flags == [(ns, (True, False)) for ns in names], flags

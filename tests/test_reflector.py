@@ -618,3 +618,26 @@ def test_401_reruns_exec_plugin_off_the_event_loop(tmp_path):
             assert svc.metrics.c["auth_refreshes"] >= 2
 
     run(body(), timeout=60)
+
+
+@pytest.mark.parametrize("engine", ["python", "native"])
+def test_relist_page_over_4mib(engine):
+    """A LIST page of 4 MiB or more is read into an anonymous mapping
+    (net/http.py _body_buffer); the Python decoder's json.loads must take it
+    (it only takes str/bytes/bytearray), or the scope never syncs."""
+    async def body():
+        async with Stack() as st:
+            f = st.factory
+            big = "x" * 20000
+            uids = []
+            for _ in range(240):  # 240 x ~24 KB: one ~5.5 MiB page
+                pod = f.running(f.new_pod())
+                pod["metadata"].setdefault("annotations", {})["blob"] = big
+                uids.append(st.srv.create(pod)["metadata"]["uid"])
+            svc = st.service({"watcher": {"engine": engine, "list_page_size": 500},
+                              "kubernetes": {"compression": False}})  # identity: the body is the mapping
+            await svc.start()
+            await st.settle(len(uids))
+            assert sorted(u for u, _, _ in st.delivered()) == sorted(uids)
+
+    run(body())

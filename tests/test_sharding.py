@@ -472,3 +472,66 @@ def test_bench_saturated_soak_mode():
     assert d["chunks"] >= 2 and d["exactly_once_all"] and d["duplicates"] == 0 and d["missing"] == 0
     assert d["events"] == d["chunks"] * 2 * 2 * 1500 and d["value"] > 0
     assert d["rss_mib"]["max"] >= d["rss_mib"]["first"] > 0
+
+
+def test_restart_owed_modified_then_deleted_namespace_ends_deleted(tmp_path):
+    """A checkpoint that still owes a MODIFIED for a pod whose namespace was
+    deleted while the watcher was down: the owed MODIFIED is re-sent first and
+    the synthesized DELETED last, so the pod does not end up live at the sink
+    (advisor round 3: the two were submitted in the opposite order)."""
+    from k8s_watcher_amd.engine.service import WatcherService
+    from k8s_watcher_amd.kube.kubeconfig import KubeEndpoint
+    from k8s_watcher_amd.metrics import Metrics
+
+    ck = str(tmp_path / "ck.bin")
+
+    async def body():
+        srv = FakeApiServer(namespaces=["stay", "gone"])
+        await srv.start()
+        sink = StubSink()
+        await sink.start()
+        s = load_settings("staging", overrides={
+            "clusterapi": {"base_url": sink.url, "health_check_on_start": False,
+                           "retry": {"delay_seconds": 30, "max_attempts": 5}},
+            "watcher": {"namespace_scope": "discover", "checkpoint": {"path": ck, "interval_seconds": 3600},
+                        "retry": {"delay_seconds": 0.05, "max_attempts": 0}}})
+        f = PodFactory(seed=9, namespaces=["stay", "gone"])
+        pod = srv.create(f.running(f.new_pod(namespace="gone")))
+        uid = pod["metadata"]["uid"]
+        srv.create(f.new_pod(namespace="stay"))
+        svc = WatcherService(s, endpoint=KubeEndpoint(server=srv.url), metrics=Metrics())
+        await svc.start()
+        await sink.state.wait_for(2, timeout=10)
+        await svc.notifier.drain(5)
+        sink.state.down = True  # the MODIFIED below stays owed (retry in 30 s)
+        srv.update(f.terminated(pod))
+        for _ in range(500):
+            if svc.metrics.c["notify_retried"] >= 1:
+                break
+            await asyncio.sleep(0.01)
+        assert svc.notifier.outstanding() == 1
+        assert await svc.checkpoint_now()
+        assert svc.last_checkpoint["checkpoint_owed"] == 1
+        svc.stop()
+        await svc.shutdown(drain_timeout=0, checkpoint=False)  # crash: the owed request dies here
+        # while down: namespace "gone" and its pods disappear
+        for key in [k for k in srv.pods if k[0] == "gone"]:
+            del srv.pods[key]
+        srv.deleted_namespaces.add("gone")
+        srv._known_ns.discard("gone")
+        sink.state.down = False
+        svc2 = WatcherService(s, endpoint=KubeEndpoint(server=srv.url), metrics=Metrics())
+        await svc2.start()
+        await sink.state.wait_for(4, timeout=10)
+        await svc2.notifier.drain(5)
+        mine = [p["event_type"] for p in sink.state.payloads() if p["uid"] == uid]
+        owed_resent = svc2.metrics.c["checkpoint_owed_resent"]
+        svc2.stop()
+        await svc2.shutdown()
+        await sink.stop()
+        await srv.stop()
+        return mine, owed_resent
+
+    mine, owed_resent = run(body(), timeout=60)
+    assert owed_resent == 1
+    assert mine == ["ADDED", "MODIFIED", "DELETED"], mine
