@@ -914,9 +914,16 @@ async def run_reference(args, fx: "Fixtures", shared: dict, targets, step: int) 
     connected = loop.create_future()
     result = {}
 
+    from k8s_watcher_amd.testing.cluster_replay import RV0
+
     def work() -> None:
+        # the clock starts at the first event of the paced step (its first
+        # resourceVersion), not when the watch connects: the live pods a new
+        # watch is sent first, and the fixture's command round trip, are not
+        # the reference's per-event work
         result["elapsed"] = ref.run(f"http://127.0.0.1:{shared['api_port']}", args.ref_events,
-                                    on_connected=lambda: loop.call_soon_threadsafe(connected.set_result, None))
+                                    on_connected=lambda: loop.call_soon_threadsafe(connected.set_result, None),
+                                    count_from_rv=RV0 + step * shared["events_per_step"])
 
     for _ in range(500):
         if int((await fx.cmd("WATCHERS"))[2]) == 0:
@@ -939,7 +946,8 @@ async def run_reference(args, fx: "Fixtures", shared: dict, targets, step: int) 
     p50 = lat[len(lat) // 2] if lat else None
     return {"events": ref.processed, "elapsed": result.get("elapsed"), "notified": ref.notified,
             "events_per_s": ref.processed / result["elapsed"] if result.get("elapsed") else None,
-            "sat_p50_ns": p50}
+            "sat_p50_ns": p50, "backlog_events": ref.backlog, "first_event_after_s": ref.first_event_after_s,
+            "cpu_seconds": ref.cpu_seconds}
 
 
 def _sum_series(per_rank: list) -> list:
@@ -1166,7 +1174,14 @@ def main(argv=None) -> int:
         "placement_rank0": res["placement"],
         "saturated_p50_latency_ms": round(sat_p50 / 1e6, 3) if sat_p50 else None,
         "reference_equiv": ({"events_per_s": round(ref_rate, 1), "events": ref["events"],
-                             "notified": ref["notified"],
+                             "notified": ref["notified"], "elapsed_s": round(ref["elapsed"], 3),
+                             "backlog_events_uncounted": ref["backlog_events"],
+                             # connect -> first paced event (fixture + control round trip; off the clock)
+                             "first_event_after_s": round(ref["first_event_after_s"], 4)
+                             if ref["first_event_after_s"] is not None else None,
+                             # the reference thread's own CPU: events per CPU-second (less noisy than wall)
+                             "events_per_cpu_s": round(ref["events"] / ref["cpu_seconds"], 1)
+                             if ref["cpu_seconds"] else None,
                              "saturated_p50_latency_ms": round(ref["sat_p50_ns"] / 1e6, 3)
                              if ref["sat_p50_ns"] else None} if ref else None),
         "baseline_source": "reference-equivalent pipeline measured in this run on the same replay "

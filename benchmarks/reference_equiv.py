@@ -75,6 +75,9 @@ class RefEquivWatcher:
         self.endpoint = sink_url.rstrip("/") + "/api/pods/update"
         self.logger = logger or logging.getLogger("watcher.pod_watcher")
         self.processed = 0
+        self.backlog = 0  # handled before the first counted event (run(count_from_rv=...))
+        self.first_event_after_s = None  # connect -> the read that brought the first counted event
+        self.cpu_seconds = None  # this thread's CPU time over the counted events
         self.notified = 0
         self.latencies_ns = []
 
@@ -132,11 +135,18 @@ class RefEquivWatcher:
             self.latencies_ns.append(time.monotonic_ns() - read_ns)
 
     def run(self, api_url: str, n_events: int, on_connected=None, warm_events: int = 0,
-            on_warm=None) -> float:
+            on_warm=None, count_from_rv: Optional[int] = None) -> float:
         """Watch until ``n_events`` pod events were handled; returns elapsed seconds
         measured from ``on_connected()`` (which should trigger the replay) or, with
         ``warm_events``, from the moment that many events were handled (then
-        ``on_warm()`` is called)."""
+        ``on_warm()`` is called).
+
+        ``count_from_rv``: events with a lower resourceVersion (what the API
+        server sends a new watch before the replay: ADDED for the pods alive
+        now) are handled but not counted, and the clock starts at the socket
+        read that brought the first event at or past it — the first paced
+        event — not at ``on_connected()``: the time the fixture takes to
+        start the replay is not the reference's."""
         u = urlsplit(api_url)
         conn = http.client.HTTPConnection(u.hostname, u.port)
         conn.request("GET", "/api/v1/pods?watch=true")
@@ -145,12 +155,16 @@ class RefEquivWatcher:
         if on_connected is not None:
             on_connected()
             t0 = time.perf_counter()
+        t_conn = t0
+        cpu0 = time.thread_time()
+        counting = count_from_rv is None
         warm = warm_events <= 0
         buf = b""
         while self.processed < n_events:
             chunk = resp.read1(65536)
             if not chunk:
                 break
+            t_read = time.perf_counter()
             read_ns = time.monotonic_ns()
             buf += chunk
             lines = buf.split(b"\n")
@@ -160,6 +174,16 @@ class RefEquivWatcher:
                     continue
                 ev = json.loads(line)
                 obj = _Model(ev["object"])
+                if not counting:
+                    rv = (ev["object"].get("metadata") or {}).get("resourceVersion")
+                    if rv is not None and int(rv) >= count_from_rv:
+                        counting = True
+                        t0 = t_read
+                        cpu0 = time.thread_time()
+                        self.first_event_after_s = t_read - t_conn
+                        self.latencies_ns.clear()
+                        self.backlog = self.processed
+                        self.processed = self.notified = 0
                 self.handle_pod_event(ev["type"], obj, read_ns)
                 self.processed += 1
                 if not warm and self.processed >= warm_events:
@@ -169,5 +193,6 @@ class RefEquivWatcher:
                         on_warm()
                     t0 = time.perf_counter()
         elapsed = time.perf_counter() - t0
+        self.cpu_seconds = time.thread_time() - cpu0
         conn.close()
         return elapsed

@@ -184,7 +184,10 @@ class ClusterModel:
             pos += len(chunk)
             ev_off[j + 1] = pos
         base_buf = np.frombuffer(b"".join(parts), dtype=np.uint8)
-        return ScopeStream(scope, base_buf, ev_off, rv_off, np.array(uid_off, dtype=np.int64), gidx, self.E)
+        sc = ScopeStream(scope, base_buf, ev_off, rv_off, np.array(uid_off, dtype=np.int64), gidx, self.E)
+        sc.pod = self.ev_pod[gidx]
+        sc.stage = self.ev_stage[gidx]
+        return sc
 
 
 class ScopeStream:
@@ -198,6 +201,9 @@ class ScopeStream:
         self.buf_step = -1
         self._rv_done = 0  # fields of buf_step patched so far (indices into rv_off / uid_off)
         self._uid_done = 0
+        self.pod: np.ndarray = np.zeros(0, dtype=np.int64)   # per local event: pod index (ClusterModel.compile)
+        self.stage: np.ndarray = np.zeros(0, dtype=np.int8)  # ... and lifecycle stage (4 = DELETED)
+        self._live: Dict[int, np.ndarray] = {}  # local prefix length -> live pods' last events
 
     _POW10 = 10 ** np.arange(RV_DIGITS - 1, -1, -1, dtype=np.int64)
     _RV_COLS = np.arange(RV_DIGITS, dtype=np.int64)
@@ -238,12 +244,43 @@ class ScopeStream:
         return memoryview(self.buf)
 
     def event_bytes(self, step: int, j: int) -> bytes:
-        a, b = int(self.ev_off[j]), int(self.ev_off[j + 1])
+        return self.range_bytes(step, j, j + 1)
+
+    def range_bytes(self, step: int, j0: int, j1: int) -> bytes:
+        """Local events [j0, j1) of ``step`` as chunk-framed bytes: one copy of
+        the base slice with its fields stamped (the shared buffer untouched)."""
+        a, b = int(self.ev_off[j0]), int(self.ev_off[j1])
         buf = self.base[a:b].copy()
         lo, hi = np.searchsorted(self.uid_off, [a, b])
-        self._patch(buf, self.rv_off[j:j + 1] - a, RV0 + step * self.E + self.gidx[j:j + 1],
+        self._patch(buf, self.rv_off[j0:j1] - a, RV0 + step * self.E + self.gidx[j0:j1],
                     self.uid_off[lo:hi] - a, step)
         return buf.tobytes()
+
+    def object_bytes(self, step: int, j: int) -> bytes:
+        """The pod object JSON of local event ``j`` of ``step`` (a LIST item)."""
+        ev = self.event_bytes(step, j)
+        body = ev[ev.index(b"\r\n") + 2:-2]
+        return body[body.index(b'"object":') + 9:-2]
+
+    def live_events(self, j1: int) -> np.ndarray:
+        """Local indices of the last event of every pod still alive after this
+        scope's events [0, j1) of one step (its ADDED sent, its DELETED not),
+        ascending. A step is always sent as a prefix, and every lifecycle
+        ends inside its step, so this is all a partly sent step leaves live.
+        Vectorised and cached per prefix: no per-event Python loop."""
+        got = self._live.get(j1)
+        if got is None:
+            if j1 <= 0:
+                got = np.zeros(0, dtype=np.int64)
+            else:
+                rev = self.pod[:j1][::-1]
+                _, first = np.unique(rev, return_index=True)
+                last = (j1 - 1 - first).astype(np.int64)  # each pod's last event in the prefix
+                got = np.sort(last[self.stage[last] != 4])
+            if len(self._live) > 64:
+                self._live.clear()
+            self._live[j1] = got
+        return got
 
     def locate(self, g0: int, g1: int) -> Tuple[int, int]:
         """Local event range of global events [g0, g1)."""
@@ -260,6 +297,8 @@ class Worker:
         self.scopes: Dict[str, ScopeStream] = {}
         self.watchers: List[Tuple[str, asyncio.StreamWriter]] = []
         self.sent: List[List[int]] = []  # [step, g0, g1) ranges of the global history sent so far
+        self.sent_end: List[int] = []    # ... the resourceVersion of each range's last event (bisect)
+        self.partial: Dict[int, int] = {}  # step -> g1 for steps sent only in part (they leave live pods)
         self.rv = RV0 - 1
 
     # ------------------------------------------------------------------ state
@@ -270,35 +309,47 @@ class Worker:
         return s
 
     def _advance(self, step: int, g0: int, g1: int) -> None:
+        E = self.m.E
         if self.sent and self.sent[-1][0] == step and self.sent[-1][2] == g0:
             self.sent[-1][2] = g1
+            self.sent_end[-1] = RV0 + step * E + g1 - 1
         else:
             self.sent.append([step, g0, g1])
-        self.rv = RV0 + step * self.m.E + g1 - 1
+            self.sent_end.append(RV0 + step * E + g1 - 1)
+        if g1 < E:
+            self.partial[step] = max(g1, self.partial.get(step, 0))
+        else:
+            self.partial.pop(step, None)
+        self.rv = RV0 + step * E + g1 - 1
 
-    def _history(self, scope: ScopeStream, since: int):
-        """(step, local index) of this scope's events sent with resourceVersion > ``since``."""
-        for step, g0, g1 in self.sent:
+    def backlog(self, scope: ScopeStream, since: int) -> List[bytes]:
+        """This scope's events sent with resourceVersion > ``since`` (a watch
+        resuming there), as a few framed byte ranges: the first range that
+        ends past ``since`` is found by bisection, and each range is one
+        vectorised copy — no per-event Python loop over the history."""
+        import bisect
+        E = self.m.E
+        out = []
+        for i in range(bisect.bisect_right(self.sent_end, since), len(self.sent)):
+            step, g0, g1 = self.sent[i]
+            g0 = max(g0, since - (RV0 + step * E) + 1)
             lo, hi = scope.locate(g0, g1)
-            for j in range(lo, hi):
-                if RV0 + step * self.m.E + int(scope.gidx[j]) > since:
-                    yield step, j
+            if hi > lo:
+                out.append(scope.range_bytes(step, lo, hi))
+        return out
+
+    def live_objects(self, scope: ScopeStream) -> List[bytes]:
+        """Object JSON of every pod alive now in this scope: O(live pods) —
+        only partly sent steps leave pods alive (``ScopeStream.live_events``)."""
+        items = []
+        for step in sorted(self.partial):
+            _, j1 = scope.locate(0, self.partial[step])
+            for j in scope.live_events(j1).tolist():
+                items.append(scope.object_bytes(step, j))
+        return items
 
     def list_body(self, name: str) -> bytes:
-        sc = self.scope(name)
-        live: Dict[int, Tuple[int, int]] = {}
-        for step, j in self._history(sc, -1):
-            g = int(sc.gidx[j])
-            key = (step, int(self.m.ev_pod[g]))
-            if self.m.ev_stage[g] == 4:
-                live.pop(key, None)
-            else:
-                live[key] = (step, j)
-        items = []
-        for step, j in live.values():
-            ev = sc.event_bytes(step, j)
-            body = ev[ev.index(b"\r\n") + 2:-2]
-            items.append(body[body.index(b'"object":') + 9:-2])
+        items = self.live_objects(self.scope(name))
         return (b'{"kind":"PodList","apiVersion":"v1","metadata":{"resourceVersion":"%d"},"items":[%s]}'
                 % (self.rv, b",".join(items)))
 
@@ -359,15 +410,12 @@ class Worker:
             since = int(rv_param) if rv_param not in (None, "", "0") else -1
             if since < 0:
                 # no resourceVersion: synthetic ADDED for the live pods (as kube-apiserver)
-                body = self.list_body(name)
-                start = body.index(b'"items":[') + 9
-                # the list items are object JSON; re-frame each as an ADDED event
-                for obj in _split_items(body[start:-2]):
+                for obj in self.live_objects(sc):
                     ev = _TYPES[0] + obj + b"}\n"
                     writer.write(b"%x\r\n%s\r\n" % (len(ev), ev))
             else:
-                for step, j in self._history(sc, since):
-                    writer.write(sc.event_bytes(step, j))
+                for data in self.backlog(sc, since):
+                    writer.write(data)
         self.watchers.append((name, writer))
 
     # ------------------------------------------------------------------ streaming
@@ -469,30 +517,6 @@ class Worker:
                 reply = str(len(self._targets()))
             out.write(reply.encode() + b"\n")
         server.close()
-
-
-def _split_items(arr: bytes) -> List[bytes]:
-    """Split the concatenated objects of a PodList ``items`` array (no nesting at top level)."""
-    out, depth, start, in_str, esc = [], 0, 0, False, False
-    for i, ch in enumerate(arr):
-        if in_str:
-            if esc:
-                esc = False
-            elif ch == 0x5C:
-                esc = True
-            elif ch == 0x22:
-                in_str = False
-        elif ch == 0x22:
-            in_str = True
-        elif ch == 0x7B:
-            if depth == 0:
-                start = i
-            depth += 1
-        elif ch == 0x7D:
-            depth -= 1
-            if depth == 0:
-                out.append(arr[start:i + 1])
-    return out
 
 
 def _cpu_list(text: str) -> set:

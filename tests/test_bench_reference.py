@@ -1,0 +1,44 @@
+"""The reference-equivalent baseline (benchmarks/reference_equiv.py) in the
+headline bench: its rate must not depend on how much history the replay
+fixture has sent before it.
+
+Round 3's fixture answered a watch without a resourceVersion by scanning every
+event ever sent in Python while the reference's clock ran, so 24 churn rounds
+per step cut the reference to two thirds of its 1-round rate and inflated
+``vs_baseline`` ~3x. Now the fixture answers from an index and the clock
+starts at the first paced event."""
+
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(rounds: int) -> dict:
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--pods-per-step", "2000", "--rounds-per-step", str(rounds), "--namespaces", "8",
+                        "--ref-events", "1500", "--latency-seconds", "0.5", "--latency-seconds-high", "0",
+                        "--staging", "off", "--apart", "off", "--no-verify", "--sink-workers", "1",
+                        "--no-placement"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])["reference_equiv"]
+
+
+def test_reference_rate_independent_of_history_length():
+    runs = {1: [], 24: []}
+    for rounds in (1, 24, 1, 24):  # interleaved: this container's load drifts
+        runs[rounds].append(_bench(rounds))
+    for ref in runs[1] + runs[24]:
+        assert ref["events"] == 1500
+        # the latency phase paced part of a step: its live pods reach the new
+        # watch as ADDED before the replay — handled, not counted
+        assert ref["backlog_events_uncounted"] > 0
+        # connect -> first paced event: the fixture's answer is O(live pods),
+        # not O(history) (round 3: seconds at 24 rounds)
+        assert ref["first_event_after_s"] < 0.5, ref
+    best = {r: max(x["events_per_s"] for x in v) for r, v in runs.items()}
+    # 24x the history, the same rate (best of two each: the shared CPU adds ~10% noise per run)
+    assert abs(best[24] - best[1]) <= 0.15 * best[1], (best, runs)
