@@ -141,6 +141,9 @@ def parse_args(argv=None):
     ap.add_argument("--sink-engine", default="auto", choices=["auto", "native", "python"],
                     help="stub clusterapi request loop (auto: native _kwcore.SinkServer unless --tls)")
     ap.add_argument("--fixture-workers", type=int, default=None, help="default 2 per rank")
+    ap.add_argument("--fixture-zero-copy", default="auto", choices=["auto", "off"],
+                    help="replay fixture sends large watch scopes with sendfile from a memfd ring (auto) "
+                         "or copies every byte into the socket (off)")
     ap.add_argument("--no-verify", dest="verify", action="store_false",
                     help="sink does not count payload keys (no exactly-once proof)")
     ap.add_argument("--latency-rate", type=float, default=100.0, help="ev/s per rank in the latency phase")
@@ -319,6 +322,7 @@ class Fixtures:
                                   "--pods", str(args.pods_per_step * world),
                                   "--namespace-list", ",".join(names), "--targets", ",".join(targets),
                                   "--workers", str(fw), "--groups", str(fronts), *api_tls,
+                                  "--zero-copy", args.fixture_zero_copy,
                                   "--notify", "critical" if args.profile == "production" else "all",
                                   *(["--group-cpus", cpu_arg] if cpu_arg else []), cpus=rank_cpus[0])
         tls_args = ["--tls-cert", self.pki.server_crt, "--tls-key", self.pki.server_key] if args.tls else []
@@ -655,6 +659,10 @@ async def rank_main(args, d: Dist) -> dict:
             prof.dump_stats(os.environ["BENCH_PROFILE"])
         cpu1 = cpu_snapshot(fx)
         cg_timed = cgroup_delta(cg0, cgroup_cpu())
+        zc = None
+        if d.rank == 0:  # the replay fixture's zero-copy sends (bytes, slot waits) so far
+            reply = await fx.cmd("ZCSTATS")
+            zc = json.loads(reply[1]) if reply and reply[0] == "ZC" else None
         pool_stats = None
         if dpool is not None:  # decode workers over the timed steps: useful lines vs idle spin/sleep
             pool1 = dpool.stats()
@@ -724,6 +732,7 @@ async def rank_main(args, d: Dist) -> dict:
                                       reverse=True)[:8],
                 "cgroup_timed": cg_timed, "cgroup_latency_high": cg_hi,
                 "decode_threads": decode_threads, "decode_pool": pool_stats, "scope": scope, "step_phases_ms": step_phases, "probe": probe, "reader": reader,
+                "fixture_zero_copy": zc,
                 "placement": {"watcher": cpu_ranges(watcher_cpus), "fixtures": cpu_ranges(fx_cpus),
                               "threads": svc.thread_placement}}
     finally:
@@ -1156,6 +1165,7 @@ def main(argv=None) -> int:
         "verify": verify,
         "per_rank": per_rank,
         "fixture_workers": res["fixture_workers"],
+        "fixture_zero_copy": res["fixture_zero_copy"],
         "front_ends": res["front_ends"],
         "sink_workers": res["sink_workers"],
         "cpu_util_rank0": res["cpu_util"],

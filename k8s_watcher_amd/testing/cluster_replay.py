@@ -39,6 +39,7 @@ Control (stdin lines → one stdout line each), forwarded to every worker::
                                controller round trip between steps) -> SENT k1-1 <events> <notifiable>
     PACE <k> <rate> <count>    first <count> events of step k at <rate>/s (0 = max) -> SENT k n m
     WATCHERS                   -> SENT - <open watch streams over all workers>
+    ZCSTATS                    -> ZC [per worker: {scope: {bytes, waits}}] (zero-copy sends)
     QUIT
 
 ``notifiable`` counts the events the production profile notifies: critical
@@ -287,13 +288,125 @@ class ScopeStream:
         return int(np.searchsorted(self.gidx, g0)), int(np.searchsorted(self.gidx, g1))
 
 
+def _sysctl_int(path: str, field: int = 0, default: int = 0) -> int:
+    try:
+        with open(path) as fh:
+            return int(fh.read().split()[field])
+    except (OSError, ValueError, IndexError):
+        return default
+
+
+def receive_queue_bound() -> int:
+    """The most data a peer socket on this host can hold unread: its receive
+    buffer — autotuned up to ``tcp_rmem[2]``, or set with SO_RCVBUF (doubled
+    by the kernel, capped at ``rmem_max``) — and no advertised window beyond it."""
+    return max(_sysctl_int("/proc/sys/net/ipv4/tcp_rmem", 2, 6 << 20),
+               2 * _sysctl_int("/proc/sys/net/core/rmem_max", 0, 4 << 20))
+
+
+def _tcp_written(sock: socket.socket) -> Optional[int]:
+    """Bytes this connection has handed to the kernel so far (acknowledged +
+    still queued), in the coordinate of ``tcpi_bytes_acked``; None if gone."""
+    import fcntl
+    import struct
+    import termios
+    try:
+        info = sock.getsockopt(socket.IPPROTO_TCP, socket.TCP_INFO, 256)
+        outq = struct.unpack("i", fcntl.ioctl(sock.fileno(), termios.TIOCOUTQ, b"\0\0\0\0"))[0]
+    except OSError:
+        return None
+    return struct.unpack_from("Q", info, 120)[0] + outq  # tcp_info.tcpi_bytes_acked
+
+
+def _tcp_acked(sock: socket.socket) -> Optional[int]:
+    import struct
+    try:
+        return struct.unpack_from("Q", sock.getsockopt(socket.IPPROTO_TCP, socket.TCP_INFO, 256), 120)[0]
+    except OSError:
+        return None
+
+
+class ZeroCopyRing:
+    """``slots`` stamped copies of one scope's step bytes in a memfd, sent with
+    ``sendfile``: the kernel references the pages instead of copying them
+    into the socket (``write`` copied every byte: at ~10 GB/s of watch
+    stream that one copy held the fixture's core).
+
+    A slot's pages stay referenced by socket buffers until the watcher has
+    read them, so a slot is re-stamped for a new step only once every
+    connection that was sent from it has had its data acknowledged past that
+    point by more than the most the peer can hold unread
+    (:func:`receive_queue_bound`): ``acked - bound >= end``. Only scopes whose
+    step is larger than that bound use a ring (the cluster-wide watch: three
+    slots, so a slot is reused two whole steps later and never waits)."""
+
+    def __init__(self, base: np.ndarray, slots: int, bound: int) -> None:
+        import mmap
+        self.n, self.slots, self.bound = len(base), slots, bound
+        self.fd = os.memfd_create("cluster-replay", getattr(os, "MFD_CLOEXEC", 0))
+        os.ftruncate(self.fd, self.n * slots)
+        self.mm = mmap.mmap(self.fd, self.n * slots)
+        arr = np.frombuffer(self.mm, dtype=np.uint8)
+        self.views = [arr[i * self.n:(i + 1) * self.n] for i in range(slots)]
+        for v in self.views:
+            v[:] = base
+        self.file = os.fdopen(os.dup(self.fd), "rb", buffering=0)
+        self.step = [-1] * slots
+        self.sent: List[List[Tuple[socket.socket, int]]] = [[] for _ in range(slots)]
+        self.next = 0
+        self.lock = asyncio.Lock()
+        self.waits = 0  # times a slot was not yet safe to re-stamp (stats)
+        self.bytes = 0
+
+    def _safe(self, i: int) -> bool:
+        for sock, end in self.sent[i]:
+            acked = _tcp_acked(sock)
+            if acked is not None and sock.fileno() >= 0 and acked - self.bound < end:
+                return False
+        return True
+
+    async def slot_for(self, sc: "ScopeStream", step: int) -> int:
+        async with self.lock:
+            if step in self.step:
+                return self.step.index(step)
+            i = self.next
+            while not self._safe(i):
+                self.waits += 1
+                await asyncio.sleep(0.0005)
+            self.next = (i + 1) % self.slots
+            self.sent[i] = []
+            self.step[i] = -1
+            v = self.views[i]
+            sc._patch(v, sc.rv_off, RV0 + step * sc.E + sc.gidx, sc.uid_off, step)
+            self.step[i] = step
+            return i
+
+    def note_sent(self, i: int, sock: socket.socket) -> None:
+        end = _tcp_written(sock)
+        if end is not None:
+            self.sent[i].append((sock, end))
+
+    def close(self) -> None:
+        self.file.close()
+        self.views = []
+        try:
+            self.mm.close()
+        except BufferError:
+            pass
+        os.close(self.fd)
+
+
 class Worker:
     """One serving process: its share of the watch connections, every command."""
 
-    def __init__(self, model: ClusterModel, sock: socket.socket, slice_bytes: int = 1 << 20) -> None:
+    def __init__(self, model: ClusterModel, sock: socket.socket, slice_bytes: int = 1 << 20,
+                 zero_copy: bool = True) -> None:
         self.m = model
         self.sock = sock
         self.slice = slice_bytes
+        self.zero_copy = zero_copy
+        self.rq_bound = receive_queue_bound() + (1 << 20)
+        self.rings: Dict[str, ZeroCopyRing] = {}
         self.scopes: Dict[str, ScopeStream] = {}
         self.watchers: List[Tuple[str, asyncio.StreamWriter]] = []
         self.sent: List[List[int]] = []  # [step, g0, g1) ranges of the global history sent so far
@@ -440,10 +553,40 @@ class Worker:
         except (ConnectionError, RuntimeError):
             pass
 
+    def ring(self, name: str, w: asyncio.StreamWriter) -> Optional[ZeroCopyRing]:
+        """The scope's zero-copy ring, when this connection can use one: plain
+        TCP (sendfile cannot go through TLS) and a step larger than the bound
+        a slot waits out (small namespace scopes keep copying)."""
+        if not self.zero_copy or w.get_extra_info("sslcontext") is not None:
+            return None
+        r = self.rings.get(name)
+        if r is None:
+            sc = self.scope(name)
+            if len(sc.base) < self.rq_bound:
+                return None
+            r = self.rings[name] = ZeroCopyRing(sc.base, 3, self.rq_bound)
+        return r
+
+    async def _send_zc(self, w: asyncio.StreamWriter, sc: ScopeStream, ring: ZeroCopyRing, k: int) -> None:
+        loop = asyncio.get_running_loop()
+        try:
+            i = await ring.slot_for(sc, k)
+            sock = w.get_extra_info("socket")
+            await loop.sendfile(w.transport, ring.file, i * ring.n, ring.n, fallback=False)
+            ring.bytes += ring.n
+            raw = getattr(sock, "_sock", sock)  # asyncio's TransportSocket wraps the socket
+            ring.note_sent(i, raw)
+        except (ConnectionError, RuntimeError, OSError):
+            pass
+
     async def step(self, k: int) -> None:
         targets = self._targets()
         self._advance(k, 0, self.m.E)  # before the first await: a watch joining now gets it as backlog
-        await asyncio.gather(*(self._send(w, self.scope(n), k) for n, w in targets))
+        sends = []
+        for n, w in targets:
+            r = self.ring(n, w)
+            sends.append(self._send_zc(w, self.scope(n), r, k) if r is not None else self._send(w, self.scope(n), k))
+        await asyncio.gather(*sends)
 
     async def pace(self, k: int, rate: float, count: int, tick: float = 0.0005) -> None:
         """The first ``count`` events of step ``k`` at ``rate`` ev/s over the whole
@@ -515,8 +658,13 @@ class Worker:
                 await self.pace(int(parts[1]), float(parts[2]), min(int(parts[3]), self.m.E))
             elif cmd == "WATCHERS":
                 reply = str(len(self._targets()))
+            elif cmd == "ZCSTATS":  # zero-copy sends: bytes, slot waits
+                reply = json.dumps({n: {"bytes": r.bytes, "waits": r.waits} for n, r in self.rings.items()},
+                                   separators=(",", ":"))
             out.write(reply.encode() + b"\n")
         server.close()
+        for r in self.rings.values():
+            r.close()
 
 
 def _cpu_list(text: str) -> set:
@@ -573,7 +721,8 @@ def run(args) -> None:
                         import ssl
                         ssl_ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
                         ssl_ctx.load_cert_chain(args.tls_cert, args.tls_key)
-                    asyncio.run(Worker(model, _reuseport_socket(ports[g], listen=True)).serve(c_r, r_w, ssl_ctx))
+                    asyncio.run(Worker(model, _reuseport_socket(ports[g], listen=True),
+                                       zero_copy=args.zero_copy == "auto").serve(c_r, r_w, ssl_ctx))
                 finally:
                     os._exit(0)
             os.close(c_r)
@@ -606,6 +755,8 @@ def run(args) -> None:
             print(f"SENT {parts[1]} {n} {model.notifiable_upto(n)}", flush=True)
         elif cmd == "WATCHERS":
             print(f"SENT - {sum(int(r) for r in replies)}", flush=True)
+        elif cmd == "ZCSTATS":
+            print("ZC " + json.dumps([json.loads(r) for r in replies], separators=(",", ":")), flush=True)
         else:
             print("OK", flush=True)
     for pid, wr, _ in workers:
@@ -635,6 +786,9 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--notify", default="critical", choices=["critical", "all"],
                     help="which events of the target namespaces count as notifiable: the production "
                          "profile's critical-events filter, or every one (development/staging)")
+    ap.add_argument("--zero-copy", default="auto", choices=["auto", "off"],
+                    help="auto: scopes whose step outgrows a peer's receive buffer are sent with sendfile "
+                         "from a memfd ring (ZeroCopyRing); off: every scope is written (copied)")
     ap.add_argument("--prototypes", type=int, default=256)
     ap.add_argument("--seed", type=int, default=0)
     run(ap.parse_args(argv))

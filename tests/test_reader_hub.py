@@ -741,3 +741,82 @@ def test_runtime_log_level_reaches_every_hub_dispatched_scope():
 
     flags = run(body(), timeout=60)
     assert flags == [(ns, (True, False)) for ns in names], flags
+
+
+def test_take_dispatch_merges_queued_reads_of_one_stream():
+    """Reads of one bound stream queued by the time the loop takes them go
+    through its pipeline as one call (GroupRead::more, engine.inc) when its
+    submits are native: the same notifications, per pod in stream order, the
+    same cache and resume RV as feeding the bytes serially — with fewer calls
+    than reads."""
+    import asyncio
+    import threading
+
+    from conftest import run
+    from test_native_pipeline import run_native
+    from k8s_watcher_amd.engine.pipeline import EventPipeline
+    from k8s_watcher_amd.metrics import Metrics
+    from k8s_watcher_amd.ops.decode import PyDecoder
+    from k8s_watcher_amd.parallel.native_notifier import NativeNotifierPool
+    from k8s_watcher_amd.testing.podgen import churn_events, event_line
+    from k8s_watcher_amd.testing.stub_sink import StubSink
+    from k8s_watcher_amd.utils.config import load_settings
+
+    data = b"".join(event_line(t, o) for t, o in churn_events(200, seed=29))
+    want_calls, want_cache, _, want_rv, _ = run_native("staging", {}, data)
+
+    async def body():
+        sink = StubSink()
+        await sink.start()
+        s = load_settings("staging", overrides={"clusterapi": {"base_url": sink.url, "health_check_on_start": False}},
+                          environ={})
+        m = Metrics()
+        pool = NativeNotifierPool(s.clusterapi, m)
+        p = EventPipeline(s, PyDecoder("staging"), pool, m)
+        p.log_events_setting = False
+        p.attach_native()
+        p.sync_native_log()
+        core = load().ReaderHub(16 * 1024, 256)
+        a, b = socket.socketpair()
+        sid = core.add(os.dup(b.fileno()))
+        core.bind(sid, p.native, True)
+        sender = threading.Thread(target=a.sendall, args=(_chunked(data),), daemon=True)
+        sender.start()
+        done = []
+        deadline = time.monotonic() + 20
+        while not done and time.monotonic() < deadline:
+            await asyncio.sleep(0.02)  # let several reads queue up before each take
+            items, _ = core.take_dispatch()
+            for sid_, buf, view, read_ns, err in items:
+                if buf == -2:
+                    p.native_result(view, read_ns)
+                    if err:
+                        done.append(sid_)
+                elif view is not None:  # after a read that needed Python: fed directly
+                    p.native_result(p.native.feed_chunked(view, read_ns), read_ns)
+                    view.release()
+                    core.release(buf)
+                    if p.native.body_done():
+                        done.append(sid_)
+            pool.flush()
+        sender.join()
+        assert await pool.drain(10)
+        got = [(x["uid"], x["event_type"]) for x in sink.state.payloads()]
+        stats = core.stats()
+        cache = {u: list(e) for u, e in p.cache.items()}
+        rv = p.native.last_rv()
+        core.unbind(sid)
+        core.close()
+        await pool.close()
+        await sink.stop()
+        a.close()
+        b.close()
+        return got, stats, cache, rv
+
+    got, stats, cache, rv = run(body(), timeout=60)
+    want = [(c[0], c[1]) for c in want_calls]
+    assert sorted(got) == sorted(want)  # exactly once
+    by_uid = lambda seq: {u: [t for uu, t in seq if uu == u] for u, _ in seq}  # noqa: E731
+    assert by_uid(got) == by_uid(want)  # per pod, in stream order
+    assert cache == {u: list(e) for u, e in want_cache.items()} and rv == want_rv
+    assert stats["merged_reads"] > 0 and stats["dispatch_batches"] < stats["reads"], stats
