@@ -126,6 +126,8 @@ def parse_args(argv=None):
                     help="watcher.validate (default payload: every raw token copied into a payload checked)")
     ap.add_argument("--hub-dispatch", default=None, choices=["on", "off"],
                     help="watcher.hub_dispatch: hub-read watches feed the native pipeline directly")
+    ap.add_argument("--partitioned-apply", default=None, choices=["on", "off"],
+                    help="watcher.partitioned_apply: a batch's apply split by pod-cache shard over the decode pool")
     ap.add_argument("--hub-framing", default=None, choices=["on", "off"],
                     help="watcher.hub_framing: the reader hub's thread de-chunks and splits bound watch bodies")
     ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
@@ -475,6 +477,7 @@ async def rank_main(args, d: Dist) -> dict:
                         **({"validate": args.validate} if args.validate else {}),
                         **({"hub_dispatch": args.hub_dispatch == "on"} if args.hub_dispatch else {}),
                         **({"hub_framing": args.hub_framing == "on"} if args.hub_framing else {}),
+                        **({"partitioned_apply": args.partitioned_apply == "on"} if args.partitioned_apply else {}),
                         **({"state_format": args.state_format} if args.state_format else {}),
                         # placement already pinned this thread (the decode workers inherit it)
                         **({"decode_affinity": args.decode_affinity or ("none" if watcher_cpus else "auto")})},
@@ -1140,6 +1143,7 @@ def main(argv=None) -> int:
                             if d.world > 1 else f"single-process ({res['scope']} watch)"),
             "engine": args.engine,
             "validate": args.validate or "payload",
+            "partitioned_apply": args.partitioned_apply or "on",
             "state_format": args.state_format or "structured",
             "decode_threads": res["decode_threads"],
             "clusterapi": "https" if args.tls else "http",

@@ -283,6 +283,8 @@ class WatcherService:
         self.pipeline = EventPipeline(s, self.decoder, self.notifier, self.metrics, cache, self.event_log,
                                       event_sharding=self._event_sharding())
         if self._native_pipeline():
+            from ..ops.native import load as _load_native
+            _load_native().set_partitioned_apply(s.watcher.partitioned_apply)
             self._decode_pool = self._make_decode_pool()
             self.pipeline.attach_native(self._decode_pool)
             http = self.api.http

@@ -2112,6 +2112,8 @@ PyMethodDef module_methods[] = {
     {"cpu_features", (PyCFunction)kw_cpu_features, METH_NOARGS, "SIMD paths in use"},
     {"set_simd", (PyCFunction)kw_set_simd, METH_O, "enable/disable the AVX2 scanner"},
     {"probe", (PyCFunction)kw_probe, METH_O, "probe(enable) -> event-loop thread time in native calls since the last call"},
+    {"set_partitioned_apply", (PyCFunction)kw_set_partitioned_apply, METH_O,
+     "set_partitioned_apply(on) -> previous: batches' apply phase split by pod-cache shard over the decode pool"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef moddef = {PyModuleDef_HEAD_INIT, "_kwcore", "native watch-event decoder", -1, module_methods};

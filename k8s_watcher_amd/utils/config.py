@@ -309,6 +309,7 @@ class WatcherSettings:
     watch_reader_max_bytes: int = 0  # ReaderHub read-ahead over all streams (0: the whole pool)
     hub_dispatch: bool = True  # hub-read watches feed the native pipeline with no Python call per read
     hub_framing: bool = True  # ... and the hub's thread de-chunks and splits their bodies (readerhub.inc HubFramer)
+    partitioned_apply: bool = True  # a batch's apply split by pod-cache shard over the decode pool (engine.inc)
     thread_pinning: str = "auto"  # auto: loop thread on its own core when the process sits in one L3 | none
     retry: RetryPolicy = field(default_factory=lambda: RetryPolicy(3, 5.0))
     watch_timeout_seconds: int = 300
@@ -489,6 +490,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         watch_reader_max_bytes=max(0, _as_int(w.get("watch_reader_max_bytes", 0), "watcher.watch_reader_max_bytes")),
         hub_dispatch=_as_bool(w.get("hub_dispatch", True), "watcher.hub_dispatch"),
         hub_framing=_as_bool(w.get("hub_framing", True), "watcher.hub_framing"),
+        partitioned_apply=_as_bool(w.get("partitioned_apply", True), "watcher.partitioned_apply"),
         malloc_trim_seconds=_bounded_float(w.get("malloc_trim_seconds", 60.0), "watcher.malloc_trim_seconds",
                                            0.0, 86400.0),
         thread_pinning=_choice(w.get("thread_pinning", "auto"), "watcher.thread_pinning", ("auto", "none")),
