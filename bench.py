@@ -574,7 +574,7 @@ async def rank_main(args, d: Dist) -> dict:
                 print(f"rank {d.rank} step {k}: {time.perf_counter() - t_start:.3f}s", file=sys.stderr)
             await d.abarrier()
 
-        async def run_stream(k0: int, steps: int, expect: int) -> None:
+        async def run_stream(k0: int, steps: int, expect: int, seconds_out: "list | None" = None) -> None:
             """``steps`` steps back to back: the fixture is handed step k+1 as soon
             as it has sent step k, so no rank idles between steps waiting for the
             slowest one; the clock still stops only when every event of every
@@ -594,7 +594,10 @@ async def rank_main(args, d: Dist) -> dict:
             t_first = t_all = t_sent = None
             next_tick = t_start + 1.0
             last_n = base
+            sec = SecondSeries(c, metrics, fx, getattr(svc, "_reader_hub", None)) if seconds_out is not None else None
             while c["events_received"] < target[0] or svc.notifier.outstanding() > 0:
+                if sec is not None:
+                    sec.tick()
                 now = time.perf_counter()
                 if now >= next_tick:  # events received in each whole second of the timed region
                     n = c["events_received"]
@@ -616,6 +619,8 @@ async def rank_main(args, d: Dist) -> dict:
                                        f"outstanding")
                 await asyncio.sleep(0.0005)
             t_end = time.perf_counter()
+            if sec is not None:
+                seconds_out.extend(sec.close())
             if sent is not None:
                 notifiable[0] += await sent
             phases.append({"first_event": (t_first or t_end) - t_start,
@@ -648,8 +653,9 @@ async def rank_main(args, d: Dist) -> dict:
         if prof is not None:
             prof.enable()
         phases.clear()
+        timed_seconds: list = []
         if args.step_sync == "stream":
-            await run_stream(args.warmup, args.steps, per_step)
+            await run_stream(args.warmup, args.steps, per_step, timed_seconds)
         else:
             for k in range(args.warmup, args.warmup + args.steps):
                 await run_step(k, per_step)
@@ -693,6 +699,7 @@ async def rank_main(args, d: Dist) -> dict:
             lat = list(metrics.latency.samples or [])
         # and at 10x that, long enough for >= 5,000 notified samples in the 20%-notifying profile
         lat_hi = []
+        lat_hi_seconds: list = []
         cg_hi = None
         if args.latency_rate_high > 0 and args.latency_seconds_high > 0:
             cg_a = cgroup_cpu()
@@ -701,7 +708,7 @@ async def rank_main(args, d: Dist) -> dict:
             count = max(1, int(args.latency_rate_high * d.world * args.latency_seconds_high))
             count = min(count, shared["events_per_step"])
             await run_latency(fx, d, svc, c, k_lat, args.latency_rate_high * d.world, count, args.step_timeout,
-                              notifiable)
+                              notifiable, seconds_out=lat_hi_seconds, metrics=metrics)
             lat_hi = list(metrics.latency.samples or [])
             cg_hi = cgroup_delta(cg_a, cgroup_cpu())
         failed = c["notify_failed"]
@@ -722,6 +729,11 @@ async def rank_main(args, d: Dist) -> dict:
                 # the reference's bench runs do: no figure against an https one)
                 ref = await run_reference(args, fx, shared, targets, k_lat + 1)
         return {"elapsed": elapsed, "events": events, "notified": notified, "series": series, "rss_mib": rss,
+                "timed_seconds": timed_seconds, "lat_hi_seconds": lat_hi_seconds,
+                "trims": {"count": c.get("malloc_trims", 0), "skipped": c.get("malloc_trims_skipped", 0),
+                          "total_ms": round(c.get("malloc_trim_us", 0) / 1e3, 2),
+                          "max_ms": round(metrics.gauges["malloc_trim_max_ms"](), 2)
+                          if "malloc_trim_max_ms" in metrics.gauges else None},
                 "gc": gc_report,
                 "events_per_step": shared["events_per_step"], "per_step_mine": per_step, "scopes": len(mine),
                 "lat": lat, "lat_hi": lat_hi, "sat": sat, "failed": failed, "ref": ref, "verify": verify,
@@ -798,12 +810,22 @@ async def run_soak(args, d, fx, svc, c, metrics, run_stream, per_step: int, noti
             "reader": reader}
 
 
-async def run_latency(fx, d, svc, c, k: int, rate: float, count: int, timeout: float, notifiable: list) -> None:
+async def run_latency(fx, d, svc, c, k: int, rate: float, count: int, timeout: float, notifiable: list,
+                      seconds_out: "list | None" = None, metrics=None) -> None:
     """Pace ``count`` events of step ``k`` at ``rate`` ev/s over the whole cluster,
-    then wait until every rank has received what it was sent and drained."""
+    then wait until every rank has received what it was sent and drained.
+    ``seconds_out``: the phase's per-second rows (:class:`SecondSeries`)."""
     sent = None
+    sec = None
+    if seconds_out is not None and metrics is not None:
+        sec = SecondSeries(c, metrics, fx, getattr(svc, "_reader_hub", None))
     if d.rank == 0:
-        sent = await fx.cmd(f"PACE {k} {rate} {count}")
+        pace = asyncio.ensure_future(fx.cmd(f"PACE {k} {rate} {count}"))
+        while not pace.done():
+            if sec is not None:
+                sec.tick()
+            await asyncio.sleep(0.0005)
+        sent = pace.result()
         notifiable[0] += int(sent[3])
     await d.abarrier()  # the fixture has sent everything
     deadline = time.monotonic() + timeout
@@ -816,8 +838,116 @@ async def run_latency(fx, d, svc, c, k: int, rate: float, count: int, timeout: f
             break
         if time.monotonic() > deadline:
             raise TimeoutError(f"rank {d.rank}: latency phase did not drain")
-        await asyncio.sleep(0.005)
+        if sec is not None:
+            sec.tick()
+        await asyncio.sleep(0.0005 if sec is not None else 0.005)
+    if sec is not None:
+        seconds_out.extend(sec.close())
     await d.abarrier()
+
+
+class SecondSeries:
+    """Per whole second of a phase, what the watcher did and what else went
+    on in that second — so a dip in the rate or a latency outlier can be tied
+    to a cause: events received; the longest
+    gap between two turns of this rank's polling coroutine (the event loop
+    was busy or blocked that long); collector pauses; ``malloc_trim`` runs
+    and their time; the loop thread's CPU; the reader hub's starved reads;
+    (rank 0) the replay and sink fixtures' CPU; and, when latency samples are
+    kept, how many arrived and the largest. ``tick()`` runs on every turn of
+    the caller's polling loop."""
+
+    def __init__(self, c, metrics, fx: "Fixtures", hub) -> None:
+        import gc
+        self.c, self.metrics, self.fx, self.hub = c, metrics, fx, hub
+        self.rows: list = []
+        self._gc_ms = 0.0
+        self._gc_max = 0.0
+        self._gc_t0 = 0.0
+        self._gc = gc
+        gc.callbacks.append(self._gc_cb)
+        now = time.perf_counter()
+        self.t_next = now + 1.0
+        self.last_tick = now
+        self.gap_max = 0.0
+        self._base = self._snap()
+
+    def _gc_cb(self, phase: str, info: dict) -> None:
+        if phase == "start":
+            self._gc_t0 = time.perf_counter()
+        else:
+            dt = (time.perf_counter() - self._gc_t0) * 1e3
+            self._gc_ms += dt
+            self._gc_max = max(self._gc_max, dt)
+
+    def _snap(self) -> dict:
+        c = self.c
+        out = {"events": c["events_received"], "trims": c.get("malloc_trims", 0), "trim_us": c.get("malloc_trim_us", 0),
+               "loop_cpu": time.thread_time(),
+               "lat_n": len(self.metrics.latency.samples) if self.metrics.latency.samples is not None else 0}
+        if self.hub is not None:
+            st = self.hub.stats()
+            out["starved"] = st.get("starved", 0)
+        if self.fx.replay is not None:
+            cpu = cpu_snapshot(self.fx, threads=False)
+            out["replay_cpu"], out["sink_cpu"] = cpu["replay"], cpu["sink"]
+        return out
+
+    def tick(self) -> None:
+        now = time.perf_counter()
+        gap = now - self.last_tick
+        self.last_tick = now
+        if gap > self.gap_max:
+            self.gap_max = gap
+        if now >= self.t_next:
+            self._row()
+            self.t_next += 1.0
+            if now >= self.t_next:  # a whole second without a turn: the gap row says so
+                self.t_next = now + 1.0
+
+    def _row(self) -> None:
+        b, a = self._snap(), self._base
+        row = {"events": b["events"] - a["events"], "loop_gap_max_ms": round(self.gap_max * 1e3, 2),
+               "loop_cpu": round(b["loop_cpu"] - a["loop_cpu"], 3),
+               "gc_ms": round(self._gc_ms, 2), "gc_max_ms": round(self._gc_max, 2),
+               "trims": b["trims"] - a["trims"], "trim_ms": round((b["trim_us"] - a["trim_us"]) / 1e3, 2)}
+        if "starved" in b:
+            row["reader_starved"] = b["starved"] - a["starved"]
+        if "replay_cpu" in b:
+            row["replay_cpu"] = round(b["replay_cpu"] - a["replay_cpu"], 3)
+            row["sink_cpu"] = round(b["sink_cpu"] - a["sink_cpu"], 3)
+        samples = self.metrics.latency.samples
+        if samples is not None and b["lat_n"] > a["lat_n"]:
+            new = samples[a["lat_n"]:b["lat_n"]]
+            row["lat_n"] = len(new)
+            row["lat_max_ms"] = round(max(new) / 1e6, 3)
+            row["lat_over_1ms"] = sum(1 for x in new if x > 1_000_000)
+        self.rows.append(row)
+        self._base = b
+        self.gap_max = 0.0
+        self._gc_ms = self._gc_max = 0.0
+
+    def close(self) -> list:
+        if self._gc_cb in self._gc.callbacks:
+            self._gc.callbacks.remove(self._gc_cb)
+        return self.rows
+
+
+def explain_seconds(rows: list, key: str = "events", low: float = 0.9) -> dict:
+    """The seconds of a series that fall below ``low`` x its median ``key``
+    (rate dips), each with what happened in it, plus the medians of the
+    explanatory columns over the whole series for comparison."""
+    if not rows:
+        return {"seconds": 0}
+    vals = sorted(r[key] for r in rows)
+    med = vals[len(vals) // 2]
+    cols = [k for k in rows[0] if k != key and isinstance(rows[0][k], (int, float))]
+    medians = {}
+    for k in cols:
+        v = sorted(r.get(k, 0) for r in rows)
+        medians[k] = v[len(v) // 2]
+    dips = [dict(r, second=i) for i, r in enumerate(rows) if med and r[key] < low * med]
+    return {"seconds": len(rows), "median_" + key: med, "medians": medians, "below": dips}
 
 
 class _GcStats:
@@ -882,7 +1012,7 @@ def cgroup_delta(a: "dict | None", b: "dict | None") -> "dict | None":
             "throttled_ms": round(d("throttled_usec") / 1e3, 1)}
 
 
-def cpu_snapshot(fx: "Fixtures") -> dict:
+def cpu_snapshot(fx: "Fixtures", threads: bool = True) -> dict:
     """CPU seconds (user+system) of this watcher process and (rank 0) of the
     replay and sink process trees — which side saturates tells what bounds a run."""
     import psutil
@@ -909,6 +1039,8 @@ def cpu_snapshot(fx: "Fixtures") -> dict:
     if fx.replay is not None:
         out["replay"] = tree(fx.replay)
         out["sink"] = sum(tree(sink) for sink in fx.sinks)
+    if not threads:
+        return out
     main = threading.get_native_id()
     for th in psutil.Process().threads():  # per thread: the event loop vs the decode workers
         out["thread_loop" if th.id == main else f"thread_{th.id}"] = th.user_time + th.system_time
@@ -1160,6 +1292,14 @@ def main(argv=None) -> int:
                                "p99_ms": round(pct(lat_hi, 99) / 1e6, 3)} if lat_hi else None),
         "timed_seconds": round(elapsed, 3),
         "rate_series": _series_stats(series),
+        # rank 0, per second of the timed steps / the 1k ev/s latency phase: what else happened
+        # in the seconds the rate dipped or a notification took > 1 ms (SecondSeries)
+        "rate_dips_rank0": explain_seconds(res["timed_seconds"]),
+        "latency_high_seconds_rank0": {"rows": res["lat_hi_seconds"],
+                                       "seconds_over_1ms": [dict(r, second=i) for i, r in
+                                                            enumerate(res["lat_hi_seconds"])
+                                                            if r.get("lat_over_1ms")]},
+        "malloc_trim_rank0": res["trims"],
         "rss_mib_rank0": ({"first": rss[0][0], "last": rss[0][-1], "max": max(rss[0])} if rss and rss[0] else None),
         "placement_apart": apart,
         "staging": staging,

@@ -333,6 +333,7 @@ class WatcherSettings:
     # native engine: every this many seconds the C heap's free pages go back to
     # the kernel (malloc_trim, off the event loop); 0 = never
     malloc_trim_seconds: float = 60.0
+    malloc_trim_min_free_mb: float = 16.0  # ... only when the C heap holds at least this much free (retained) memory
     shard: "ShardSettings" = field(default_factory=lambda: ShardSettings())
     leader_election: LeaderElectionSettings = field(default_factory=LeaderElectionSettings)
 
@@ -493,6 +494,8 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         partitioned_apply=_as_bool(w.get("partitioned_apply", True), "watcher.partitioned_apply"),
         malloc_trim_seconds=_bounded_float(w.get("malloc_trim_seconds", 60.0), "watcher.malloc_trim_seconds",
                                            0.0, 86400.0),
+        malloc_trim_min_free_mb=_bounded_float(w.get("malloc_trim_min_free_mb", 16.0), "watcher.malloc_trim_min_free_mb",
+                                               0.0, 1e6),
         thread_pinning=_choice(w.get("thread_pinning", "auto"), "watcher.thread_pinning", ("auto", "none")),
         retry=_retry(w.get("retry"), "watcher.retry", RetryPolicy(3, 5.0), min_attempts=0),
         watch_timeout_seconds=_as_int(w.get("watch_timeout_seconds", 300), "watcher.watch_timeout_seconds"),
