@@ -52,6 +52,9 @@ def parse_args(argv=None):
     ap.add_argument("--concurrency", type=int, default=16, help="watcher.relist_concurrency")
     ap.add_argument("--page", type=int, default=500, help="watcher.list_page_size")
     ap.add_argument("--decode-threads", default="auto")
+    ap.add_argument("--initial-sync", default="list", choices=["list", "watch_list"],
+                    help="watcher.initial_sync: LIST pages, or a WatchList stream (sendInitialEvents) — "
+                         "both the initial sync and the post-410 resync")
     ap.add_argument("--sink-workers", type=int, default=2)
     ap.add_argument("--timeout", type=float, default=300.0)
     ap.add_argument("--json-out", default=None)
@@ -161,7 +164,8 @@ async def main_async(args) -> dict:
             "watcher": {"engine": "native", "log_level": "WARNING", "retry": {"max_attempts": 0, "delay_seconds": 0.05},
                         "namespace_scope": "discover" if args.scope == "discover" else "client",
                         "list_page_size": args.page, "relist_slice_ms": args.slice_ms,
-                        "relist_concurrency": args.concurrency, "decode_threads": args.decode_threads}},
+                        "relist_concurrency": args.concurrency, "decode_threads": args.decode_threads,
+                        "initial_sync": args.initial_sync}},
             environ={})
         metrics = Metrics()
         c = metrics.c
@@ -228,7 +232,8 @@ async def main_async(args) -> dict:
             "benchmark": "relist_storm",
             "config": {"namespaces": args.namespaces, "pods": info["pods"], "scope": args.scope, "scopes": scopes,
                        "churn": args.churn, "relist_slice_ms": args.slice_ms, "relist_concurrency": args.concurrency,
-                       "list_page_size": args.page, "profile": "staging", "engine": "native"},
+                       "list_page_size": args.page, "profile": "staging", "engine": "native",
+                       "initial_sync": args.initial_sync},
             "fixture_setup_s": round(fixture_s, 2),
             "initial": {"wall_s": round(initial_s, 3), "watcher_cpu_s": cpu(cpu0, cpu1), "loop_lag": initial_lag,
                         "relist": slices(initial_slices), "exactly_once": initial_ok, "notified": len(keys0)},

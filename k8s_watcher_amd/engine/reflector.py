@@ -31,6 +31,7 @@ This reflector:
 from __future__ import annotations
 
 import asyncio
+import json
 import logging
 import time
 from typing import Optional
@@ -269,9 +270,86 @@ class Reflector:
         end: list = []
         framed = [False]
         errors: list = []
+        pipe = self.pipeline
+        native = pipe.native
+        rl = wl = None
+        t_busy = time.monotonic()
+        if native is not None:
+            # native: the initial events go into a Relist as they arrive, read
+            # by read (ops/csrc/relist.inc, WatchList): no Python object per
+            # pod and no whole-state reconcile at the end — only the sweep of
+            # the cached pods the stream did not contain, in slices
+            from ..ops.native import load
+            wl = load().WatchList()
+            rl = native.relist(self.namespace if self._scoped() else None, notify)
 
         def on_mode(is_framed: bool) -> None:
             framed[0] = is_framed
+
+        # native: the sink only cuts each read into segments (C++, no Python
+        # object per pod) and queues them; the coroutine below applies them in
+        # watcher.relist_slice_ms slices with the loop free in between, and
+        # the socket stops being read while more than this is queued
+        queue: list = []  # [(segments, read_ns)]
+        queued = [0]
+        backlog_limit = max(8 << 20, 2 * (w.watch_read_bytes or (4 << 20)))
+        wake = asyncio.Event()
+        held = [False]
+        stream_done = [False]
+
+        def sink_native(data: bytes, read_ns: int) -> None:
+            if stream_done[0]:
+                return
+            segs = wl.feed(data, framed[0])
+            queue.append((segs, read_ns))
+            for kind, payload in segs:
+                if kind <= 1:
+                    queued[0] += len(payload)
+                elif kind in (2, 3):
+                    stream_done[0] = True
+            wake.set()
+            if stream_done[0] and self.stream is not None:
+                self.stream.close()
+            elif queued[0] > backlog_limit and not held[0] and self.stream is not None:
+                held[0] = True
+                self.stream._proto.set_reading(False)
+
+        async def apply_queued() -> None:
+            budget_us = w.relist_slice_ms * 1000.0
+            while queue and not end and not errors:
+                segs, read_ns = queue.pop(0)
+                for kind, payload in segs:
+                    if kind == 0:  # ADDED / MODIFIED objects of one read: a Relist page
+                        rl.page(payload)
+                        while True:
+                            done, ctrl = pipe.native_slice(rl.step, budget_us, read_ns)
+                            for ev in ctrl:
+                                self._handle_control(ev)
+                            if done:
+                                break
+                            await asyncio.sleep(0)
+                        queued[0] -= len(payload)
+                    elif kind == 1:  # DELETED during the initial events: the watch path
+                        for ev in pipe.native_result(native.feed(payload, read_ns), read_ns):
+                            self._handle_control(ev)
+                        queued[0] -= len(payload)
+                    elif kind == 2:
+                        try:
+                            errors.append(json.loads(payload) or {})
+                        except ValueError:
+                            errors.append({"message": "undecodable ERROR event"})
+                    elif kind == 3:
+                        end.append(payload)
+                    else:
+                        self.metrics.c["events_invalid"] += 1
+                        self.log.warning(f"Skipping undecodable watch line (INVALID): {payload}")
+                    if end or errors:
+                        break
+                if held[0] and queued[0] <= backlog_limit // 2 and self.stream is not None:
+                    held[0] = False
+                    if not self._paused:
+                        self.stream._proto.set_reading(True)
+                await asyncio.sleep(0)
 
         def sink(data: bytes, read_ns: int) -> None:
             if end or errors:
@@ -297,7 +375,7 @@ class Reflector:
 
         try:
             self.stream = await self.api.watch_pods(
-                sink, namespace=self.namespace, send_initial_events=True,
+                sink_native if wl is not None else sink, namespace=self.namespace, send_initial_events=True,
                 label_selector=w.label_selector, field_selector=w.field_selector,
                 raw_chunked=True, on_mode=on_mode)
         except ApiError as exc:
@@ -310,6 +388,21 @@ class Reflector:
         try:
             finished = self.stream.finished
             idle = w.watch_list_idle_seconds
+            if wl is not None:
+                while not end and not errors and not self._stop.is_set():
+                    if queue:
+                        await apply_queued()
+                        continue
+                    if finished.done():
+                        break
+                    wake.clear()
+                    waiter = asyncio.ensure_future(wake.wait())
+                    await asyncio.wait([finished, waiter], timeout=min(1.0, idle),
+                                       return_when=asyncio.FIRST_COMPLETED)
+                    waiter.cancel()
+                    if (not queue and not finished.done() and not end and not held[0]
+                            and time.monotonic() - self.stream.last_activity > idle):
+                        raise WatchListUnsupported(f"no initial-events-end bookmark after {idle}s idle")
             while not finished.done() and not end and not errors and not self._stop.is_set():
                 await asyncio.wait([finished], timeout=min(1.0, idle))
                 if (not finished.done() and not end
@@ -333,12 +426,31 @@ class Reflector:
         self.metrics.c["relists"] += 1
         self.metrics.c["watch_list_syncs"] += 1
         read_ns = time.monotonic_ns()
-        ctrl = self.pipeline.reconcile(list(state.values()), read_ns, notify=notify,
-                                       scope_ns=self.namespace if self._scoped() else None)
-        for ev in ctrl:
-            self._handle_control(ev)
+        if rl is not None:
+            # the scope's cached pods the initial events did not contain: DELETED, in slices
+            budget_us = w.relist_slice_ms * 1000.0
+            while True:
+                done, ctrl = pipe.native_slice(rl.sweep, budget_us, read_ns)
+                for ev in ctrl:
+                    self._handle_control(ev)
+                if done:
+                    break
+                await asyncio.sleep(0)
+            st = rl.stats()
+            c = self.metrics.c
+            c["relist_items"] += st["listed"]
+            c["relist_unchanged"] += st["unchanged"]
+            c["relist_deleted"] += st["deleted"]
+            self.last_relist = dict(st, wall_s=time.monotonic() - t_busy, scope=self.scope, watch_list=wl.stats())
+        else:
+            ctrl = self.pipeline.reconcile(list(state.values()), read_ns, notify=notify,
+                                           scope_ns=self.namespace if self._scoped() else None)
+            for ev in ctrl:
+                self._handle_control(ev)
         self.rv = end[0]
         self.pipeline.last_rv = end[0]
+        if native is not None:
+            native.set_last_rv(end[0])
         self.synced.set()
 
     def _scoped(self) -> bool:

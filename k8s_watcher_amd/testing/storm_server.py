@@ -130,6 +130,7 @@ class StormServer:
         self.ns_watches: List[asyncio.StreamWriter] = []
         self.lists = 0
         self.list_bytes = 0
+        self.watch_lists = 0
 
     def list_page(self, scope: str, limit: Optional[int], cont: Optional[str]) -> Tuple[int, bytes]:
         keys = self.c.keys(scope)
@@ -182,6 +183,14 @@ class StormServer:
                     if watch:
                         rv = q.get("resourceVersion")
                         writer.write(_HDR)
+                        if q.get("sendInitialEvents", "").lower() == "true":
+                            # WatchList (KEP-3157): the scope's pods as ADDED, then the
+                            # initial-events-end bookmark, then the live watch
+                            await self.initial_events(scope, writer)
+                            self.watch_lists += 1
+                            self.pod_watches.append((scope, writer))
+                            await reader.read()
+                            return
                         if rv and rv != "0" and int(rv) < self.c.compacted:
                             err = json.dumps({"type": "ERROR", "object": {
                                 "kind": "Status", "apiVersion": "v1", "status": "Failure", "code": 410,
@@ -206,6 +215,27 @@ class StormServer:
             self.pod_watches = [(s, w) for s, w in self.pod_watches if w is not writer]
             self.ns_watches = [w for w in self.ns_watches if w is not writer]
             writer.close()
+
+    async def initial_events(self, scope: str, writer: asyncio.StreamWriter) -> None:
+        """ADDED for every pod of the scope (one chunk per event, as the API
+        server writes them), sent in ~1 MiB slices, then the bookmark."""
+        buf = []
+        size = 0
+        for k in list(self.c.keys(scope)):
+            ent = self.c.pods.get(k)
+            if ent is None:
+                continue
+            buf.append(_chunk(b'{"type":"ADDED","object":' + ent[4] + b"}\n"))
+            size += len(buf[-1])
+            if size >= (1 << 20):
+                writer.write(b"".join(buf))
+                buf, size = [], 0
+                await writer.drain()
+        bm = {"type": "BOOKMARK", "object": {"kind": "Pod", "apiVersion": "v1", "metadata": {
+            "resourceVersion": str(self.c.rv), "annotations": {"k8s.io/initial-events-end": "true"}}}}
+        buf.append(_chunk(json.dumps(bm, separators=(",", ":")).encode() + b"\n"))
+        writer.write(b"".join(buf))
+        await writer.drain()
 
     def expire(self) -> int:
         self.c.rv += 1  # the compaction's own revision: every watch is now behind it
@@ -249,7 +279,8 @@ async def serve(args) -> None:
         elif cmd == "EXPIRE":
             reply = {"expired": srv.expire()}
         elif cmd == "STATS":
-            reply = {"lists": srv.lists, "list_bytes": srv.list_bytes, "pod_watches": len(srv.pod_watches),
+            reply = {"lists": srv.lists, "list_bytes": srv.list_bytes, "watch_lists": srv.watch_lists,
+                     "pod_watches": len(srv.pod_watches),
                      "rv": cluster.rv, "pods": len(cluster.pods)}
         else:
             reply = {"error": f"unknown command {cmd}"}
