@@ -108,20 +108,25 @@ def test_launcher_two_shards_exactly_once(tmp_path):
     assert "Shard 0/2" in err and "Shard 1/2" in err
 
 
-@pytest.mark.parametrize("ranks", [2, 4])
-def test_bench_sharded_ranks_exactly_once(ranks):
+@pytest.mark.parametrize("ranks,assignment,decode", [(2, "balanced", "0"), (4, "balanced", "0"), (4, "hash", "0"),
+                                                     (8, "balanced", "auto")])
+def test_bench_sharded_ranks_exactly_once(ranks, assignment, decode):
     """bench.py --gpus N is the product's sharded scale-out: N shard processes
     (gloo ranks) against ONE cluster fixture; each watches only the namespaces
-    it owns, the shared verify-mode sink proves the union is exactly-once."""
+    it owns, the shared verify-mode sink proves the union is exactly-once.
+    N=8 is the driver's node shape (with decode_threads: auto sizing each
+    rank from its share of this container's CPUs); ``hash`` is the loss-free
+    assignment for dynamic namespace sets (parallel/shard.py)."""
     port = free_port()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", BENCH_DEBUG="1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
                         "--gpus", str(ranks), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off", "--pods-per-step", "300",
                         "--namespaces", "16", "--ref-events", "0", "--latency-seconds", "0.5", "--latency-seconds-high", "0.5",
-                        "--sink-workers", "2", "--fixture-workers", "2", "--no-placement",
-                        "--decode-threads", "0", "--step-timeout", "45"],
-                       capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+                        "--sink-workers", "2" if ranks < 8 else "1", "--fixture-workers", "2" if ranks < 8 else "1",
+                        "--no-placement", "--assignment", assignment,
+                        "--decode-threads", decode, "--step-timeout", "90"],
+                       capture_output=True, text=True, timeout=900, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1  # rank 0 only
@@ -132,7 +137,12 @@ def test_bench_sharded_ranks_exactly_once(ranks):
     assert d["front_ends"] == ranks  # one API-server and one clusterapi front-end per rank, one cluster
     # every shard watched its own namespaces: 16 in total, split evenly, each event counted once
     assert sum(p["scopes"] for p in d["per_rank"]) == 16, d["per_rank"]
-    assert {p["scopes"] for p in d["per_rank"]} == {16 // ranks}, d["per_rank"]
+    if assignment == "balanced":
+        assert {p["scopes"] for p in d["per_rank"]} == {16 // ranks}, d["per_rank"]
+    assert f"assignment={assignment}" in d["config"]["parallelism"]
+    if decode == "auto":  # 8 local ranks share this container's CPUs: no rank plans more than its share
+        from k8s_watcher_amd.utils.cpus import available_cpus
+        assert d["config"]["decode_threads"] <= max(0, available_cpus() // ranks - 2)
     assert sum(p["events"] for p in d["per_rank"]) == 2 * ranks * 1500, (d["per_rank"], r.stderr[-3000:])
     v = d["verify"]
     assert v["exactly_once"] and v["duplicates"] == 0 and v["missing"] == 0, (v, r.stderr[-3000:])
