@@ -32,19 +32,42 @@ def test_malloc_trim_setting():
         load_settings("production", overrides={"watcher": {"malloc_trim_seconds": -1}}, environ={})
 
 
-def test_service_trims_periodically():
-    """The service's trim loop runs the trim off the event loop and counts it."""
-    from k8s_watcher_amd.engine.service import WatcherService
-    from k8s_watcher_amd.metrics import Metrics
+def _trim_stub(min_free_mb):
+    import types
 
-    class Stub:
-        metrics = Metrics()
+    from k8s_watcher_amd.metrics import Metrics
+    return types.SimpleNamespace(metrics=Metrics(), log=__import__("logging").getLogger("test"),
+                                 settings=types.SimpleNamespace(watcher=types.SimpleNamespace(
+                                     malloc_trim_min_free_mb=min_free_mb)))
+
+
+def test_service_trims_periodically():
+    """The service's trim loop runs the trim off the event loop, counts and times it."""
+    from k8s_watcher_amd.engine.service import WatcherService
 
     async def body():
-        stub = Stub()
+        stub = _trim_stub(0.0)
         task = asyncio.ensure_future(WatcherService._malloc_trim_loop(stub, 0.01))
         await asyncio.sleep(0.2)
         task.cancel()
-        return stub.metrics.c.get("malloc_trims", 0)
+        return stub.metrics
 
-    assert asyncio.run(body()) >= 2
+    m = asyncio.run(body())
+    assert m.c.get("malloc_trims", 0) >= 2
+    assert m.c["malloc_trim_us"] > 0 and m.gauges["malloc_trim_max_ms"]() >= m.gauges["malloc_trim_last_ms"]() > 0
+
+
+def test_service_skips_trim_below_free_threshold():
+    """watcher.malloc_trim_min_free_mb: no trim (no arena walk under their
+    locks) while the heap retains less free memory than that."""
+    from k8s_watcher_amd.engine.service import WatcherService
+
+    async def body():
+        stub = _trim_stub(1e6)  # a terabyte: never reached
+        task = asyncio.ensure_future(WatcherService._malloc_trim_loop(stub, 0.01))
+        await asyncio.sleep(0.15)
+        task.cancel()
+        return stub.metrics
+
+    m = asyncio.run(body())
+    assert m.c.get("malloc_trims", 0) == 0 and m.c["malloc_trims_skipped"] >= 2
