@@ -423,8 +423,6 @@ class Reflector:
             if self._stop.is_set():
                 return
             raise HttpError("watch-list stream ended before the initial events were complete")
-        self.metrics.c["relists"] += 1
-        self.metrics.c["watch_list_syncs"] += 1
         read_ns = time.monotonic_ns()
         if rl is not None:
             # the scope's cached pods the initial events did not contain: DELETED, in slices
@@ -447,6 +445,9 @@ class Reflector:
                                            scope_ns=self.namespace if self._scoped() else None)
             for ev in ctrl:
                 self._handle_control(ev)
+        # counted once the whole state is applied, sweep included (what waits on them sees a finished sync)
+        self.metrics.c["relists"] += 1
+        self.metrics.c["watch_list_syncs"] += 1
         self.rv = end[0]
         self.pipeline.last_rv = end[0]
         if native is not None:
