@@ -824,7 +824,7 @@ async def run_latency(fx, d, svc, c, k: int, rate: float, count: int, timeout: f
         while not pace.done():
             if sec is not None:
                 sec.tick()
-            await asyncio.sleep(0.0005)
+            await asyncio.sleep(0.002)
         sent = pace.result()
         notifiable[0] += int(sent[3])
     await d.abarrier()  # the fixture has sent everything
@@ -840,7 +840,7 @@ async def run_latency(fx, d, svc, c, k: int, rate: float, count: int, timeout: f
             raise TimeoutError(f"rank {d.rank}: latency phase did not drain")
         if sec is not None:
             sec.tick()
-        await asyncio.sleep(0.0005 if sec is not None else 0.005)
+        await asyncio.sleep(0.002 if sec is not None else 0.005)  # the watcher's loop: few extra wake-ups
     if sec is not None:
         seconds_out.extend(sec.close())
     await d.abarrier()

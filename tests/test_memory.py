@@ -48,7 +48,7 @@ def test_service_trims_periodically():
     async def body():
         stub = _trim_stub(0.0)
         task = asyncio.ensure_future(WatcherService._malloc_trim_loop(stub, 0.01))
-        await asyncio.sleep(0.2)
+        await asyncio.sleep(0.8)  # each trim waits for a quiet quarter second first
         task.cancel()
         return stub.metrics
 
@@ -71,3 +71,22 @@ def test_service_skips_trim_below_free_threshold():
 
     m = asyncio.run(body())
     assert m.c.get("malloc_trims", 0) == 0 and m.c["malloc_trims_skipped"] >= 2
+
+
+def test_service_defers_trim_under_load():
+    """Under sustained traffic the trim waits for a quiet moment (the freed
+    pages would be reused at once, and a trim stalls allocating threads)."""
+    from k8s_watcher_amd.engine.service import WatcherService
+
+    async def body():
+        stub = _trim_stub(0.0)
+        task = asyncio.ensure_future(WatcherService._malloc_trim_loop(stub, 0.05))
+        t_end = asyncio.get_running_loop().time() + 0.9
+        while asyncio.get_running_loop().time() < t_end:  # ~20k events/s
+            stub.metrics.c["events_received"] += 100
+            await asyncio.sleep(0.005)
+        task.cancel()
+        return stub.metrics
+
+    m = asyncio.run(body())
+    assert m.c.get("malloc_trims", 0) == 0 and m.c["malloc_trims_deferred"] >= 1
