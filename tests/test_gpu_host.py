@@ -121,3 +121,33 @@ def test_sharded_ha_and_spool_paths_on_host(tmp_path):
     import test_spool
     test_ha_soak.test_graceful_handover_under_churn_keeps_final_state(tmp_path / "ha")
     test_spool.test_shutdown_with_owed_notifications_spools_then_checkpoints(tmp_path / "sp")
+
+
+def test_round4_paths_on_host():
+    """Round 4's paths on the host's cores: the partitioned apply against the
+    serial one (every profile), queued reads merged into one pipeline call, a
+    bench run at the driver's shape with the zero-copy replay fixture and the
+    partitioned apply (exactly-once, both ran), and a WatchList storm through
+    the native relist."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import test_partitioned_apply
+    import test_reader_hub
+    for env, ov in test_partitioned_apply.PROFILES:
+        test_partitioned_apply.test_partitioned_apply_matches_serial(env, ov)
+    test_reader_hub.test_take_dispatch_merges_queued_reads_of_one_stream()
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+                          "--rounds-per-step", "4", "--apart", "off", "--staging", "off", "--ref-events", "0",
+                          "--latency-seconds", "0", "--latency-seconds-high", "2", "--probe"],
+                         capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["verify"]["exactly_once"] and line["config"]["partitioned_apply"] == "on"
+    assert line["loop_probe_rank0"]["partitioned_batches"] > 0
+    assert sum(s.get("*", {}).get("bytes", 0) for s in line["fixture_zero_copy"]) > 0
+    assert line["latency_high_seconds_rank0"]["rows"] and "rate_dips_rank0" in line
+    res = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "relist_storm.py"), "--scope", "cluster",
+                          "--namespaces", "16", "--pods", "20000", "--churn", "300", "--initial-sync", "watch_list"],
+                         capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
+    d = json.loads(res.stdout.strip().splitlines()[-1])
+    assert d["initial"]["exactly_once"] and d["storm"]["exactly_once"] and d["server"]["lists"] == 0
