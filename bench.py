@@ -143,9 +143,9 @@ def parse_args(argv=None):
     ap.add_argument("--sink-engine", default="auto", choices=["auto", "native", "python"],
                     help="stub clusterapi request loop (auto: native _kwcore.SinkServer unless --tls)")
     ap.add_argument("--fixture-workers", type=int, default=None, help="default 2 per rank")
-    ap.add_argument("--fixture-zero-copy", default="auto", choices=["auto", "cold", "off"],
-                    help="replay fixture sends large watch scopes with sendfile from a memfd ring, each slice "
-                         "read into the cache first (auto) or not (cold), or copies every byte into the socket (off)")
+    ap.add_argument("--fixture-zero-copy", default="auto", choices=["auto", "warm", "off"],
+                    help="replay fixture sends large watch scopes with sendfile from a memfd ring (auto), each "
+                         "slice read into the cache first (warm), or copies every byte into the socket (off)")
     ap.add_argument("--no-verify", dest="verify", action="store_false",
                     help="sink does not count payload keys (no exactly-once proof)")
     ap.add_argument("--latency-rate", type=float, default=100.0, help="ev/s per rank in the latency phase")

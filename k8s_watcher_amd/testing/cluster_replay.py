@@ -401,7 +401,7 @@ class Worker:
     """One serving process: its share of the watch connections, every command."""
 
     def __init__(self, model: ClusterModel, sock: socket.socket, slice_bytes: int = 1 << 20,
-                 zero_copy: bool = True, warm: bool = True) -> None:
+                 zero_copy: bool = True, warm: bool = False) -> None:
         self.m = model
         self.sock = sock
         self.slice = slice_bytes
@@ -740,7 +740,7 @@ def run(args) -> None:
                         ssl_ctx.load_cert_chain(args.tls_cert, args.tls_key)
                     asyncio.run(Worker(model, _reuseport_socket(ports[g], listen=True),
                                        zero_copy=args.zero_copy != "off",
-                                       warm=args.zero_copy == "auto").serve(c_r, r_w, ssl_ctx))
+                                       warm=args.zero_copy == "warm").serve(c_r, r_w, ssl_ctx))
                 finally:
                     os._exit(0)
             os.close(c_r)
@@ -804,10 +804,11 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--notify", default="critical", choices=["critical", "all"],
                     help="which events of the target namespaces count as notifiable: the production "
                          "profile's critical-events filter, or every one (development/staging)")
-    ap.add_argument("--zero-copy", default="auto", choices=["auto", "cold", "off"],
+    ap.add_argument("--zero-copy", default="auto", choices=["auto", "warm", "off"],
                     help="auto: scopes whose step outgrows a peer's receive buffer are sent with sendfile "
-                         "from a memfd ring (ZeroCopyRing), each slice read through first so it leaves from "
-                         "cache; cold: the same without that read; off: every scope is written (copied)")
+                         "from a memfd ring (ZeroCopyRing); warm: each slice is read through first so it "
+                         "leaves from cache (moves ~0.45 core of the receiver's cold copy to the fixture, "
+                         "profiles/r4/zero_copy_gpu_box.md); off: every scope is written (copied)")
     ap.add_argument("--prototypes", type=int, default=256)
     ap.add_argument("--seed", type=int, default=0)
     run(ap.parse_args(argv))
