@@ -109,7 +109,7 @@ def parse_args(argv=None):
     ap.add_argument("--watch-reader", default=None, choices=["native", "asyncio"], help="watcher.watch_reader")
     ap.add_argument("--watch-reader-buffers", type=int, default=None, help="watcher.watch_reader_buffers")
     ap.add_argument("--watch-reader-max-bytes", type=int, default=None, help="watcher.watch_reader_max_bytes")
-    ap.add_argument("--thread-pinning", default=None, choices=["auto", "none"], help="watcher.thread_pinning")
+    ap.add_argument("--thread-pinning", default=None, choices=["auto", "loop", "none"], help="watcher.thread_pinning")
     ap.add_argument("--no-placement", dest="placement", action="store_false",
                     help="no per-rank L3 domain assignment (each watcher still pins per watcher.decode_affinity)")
     ap.add_argument("--front-ends", default="per-rank", choices=["per-rank", "shared"],
@@ -440,10 +440,14 @@ async def rank_main(args, d: Dist) -> dict:
         # by default the fixtures run on the watchers' own L3 domains
         fx_cpus = fixture_cpus(all_cpus, held) if held else all_cpus
     elif watcher_cpus and args.thread_pinning != "none":
-        # ... minus the physical core watcher.thread_pinning gives the event-loop thread
-        from k8s_watcher_amd.utils.cpus import loop_core_split
+        # ... minus the physical cores watcher.thread_pinning gives the event-loop
+        # thread (and, with auto, the reader thread)
+        from k8s_watcher_amd.utils.cpus import loop_core_split, reader_core_split
         split = loop_core_split(watcher_cpus)
         fx_cpus = split[1] if split else None
+        if fx_cpus and args.thread_pinning in (None, "auto"):
+            rsplit = reader_core_split(fx_cpus)
+            fx_cpus = rsplit[1] if rsplit else fx_cpus
     elif watcher_cpus:
         fx_cpus = set(watcher_cpus)
     rank_fx = d.all_gather(sorted(fx_cpus) if fx_cpus else None)  # each rank's front-ends run here

@@ -532,9 +532,10 @@ class WatcherService:
         thread are pinned to the rest. The loop thread itself stays free to
         move — pinned hard, it could not escape another process scheduled on
         its core, and the latency tail grew to ~10 ms (profiles/latency_curve_*)."""
-        if self.settings.watcher.thread_pinning != "auto":
+        mode = self.settings.watcher.thread_pinning
+        if mode == "none":
             return
-        from ..utils.cpus import loop_core_split
+        from ..utils.cpus import loop_core_split, reader_core_split
         try:
             split = loop_core_split(os.sched_getaffinity(0))
         except (AttributeError, OSError):
@@ -543,9 +544,19 @@ class WatcherService:
             return
         loop_cpus, rest = split
         tids = list(self._decode_pool.thread_ids()) if self._decode_pool else []
-        if self._reader_hub is not None:
-            tids.append(self._reader_hub.core.thread_id())
+        reader_cpus = None
+        reader_tid = self._reader_hub.core.thread_id() if self._reader_hub is not None else 0
+        if reader_tid and mode == "auto":
+            # the reader thread gets a core of its own too: it copies the watch
+            # bodies out of the kernel and bounds the single-stream rate
+            rsplit = reader_core_split(rest)
+            if rsplit is not None:
+                reader_cpus, rest = rsplit
+        if reader_tid and reader_cpus is None:
+            tids.append(reader_tid)
         try:
+            if reader_cpus is not None:
+                os.sched_setaffinity(reader_tid, reader_cpus)
             for tid in tids:
                 if tid:
                     os.sched_setaffinity(tid, rest)
@@ -557,7 +568,8 @@ class WatcherService:
         except OSError as exc:
             self.log.warning(f"Thread pinning skipped: {exc}")
             return
-        self.thread_placement = {"loop": sorted(loop_cpus), "workers": sorted(rest)}
+        self.thread_placement = {"loop": sorted(loop_cpus), "workers": sorted(rest),
+                                 **({"reader": sorted(reader_cpus)} if reader_cpus is not None else {})}
         self.log.info(f"CPUs {sorted(loop_cpus)} kept for the event-loop thread; {len(tids)} worker threads on the rest")
 
     def _native_pipeline(self) -> bool:

@@ -310,7 +310,7 @@ class WatcherSettings:
     hub_dispatch: bool = True  # hub-read watches feed the native pipeline with no Python call per read
     hub_framing: bool = True  # ... and the hub's thread de-chunks and splits their bodies (readerhub.inc HubFramer)
     partitioned_apply: bool = True  # a batch's apply split by pod-cache shard over the decode pool (engine.inc)
-    thread_pinning: str = "auto"  # auto: loop thread on its own core when the process sits in one L3 | none
+    thread_pinning: str = "auto"  # auto: loop thread and reader thread on cores of their own in one L3 | loop | none
     retry: RetryPolicy = field(default_factory=lambda: RetryPolicy(3, 5.0))
     watch_timeout_seconds: int = 300
     list_page_size: int = 500
@@ -496,7 +496,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
                                            0.0, 86400.0),
         malloc_trim_min_free_mb=_bounded_float(w.get("malloc_trim_min_free_mb", 16.0), "watcher.malloc_trim_min_free_mb",
                                                0.0, 1e6),
-        thread_pinning=_choice(w.get("thread_pinning", "auto"), "watcher.thread_pinning", ("auto", "none")),
+        thread_pinning=_choice(w.get("thread_pinning", "auto"), "watcher.thread_pinning", ("auto", "loop", "none")),
         retry=_retry(w.get("retry"), "watcher.retry", RetryPolicy(3, 5.0), min_attempts=0),
         watch_timeout_seconds=_as_int(w.get("watch_timeout_seconds", 300), "watcher.watch_timeout_seconds"),
         list_page_size=max(1, _as_int(w.get("list_page_size", 500), "watcher.list_page_size")),

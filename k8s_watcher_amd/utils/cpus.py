@@ -290,6 +290,27 @@ def core_siblings(cpu: int, root: str = "") -> set:
         return {cpu}
 
 
+def reader_core_split(rest: set, min_cores: int = 4, root: str = "") -> Optional[tuple]:
+    """``(reader_cpus, worker_cpus)``: the lowest physical core of ``rest``
+    (what :func:`loop_core_split` left) for the reader hub's thread, the rest
+    for the decode workers. With the watch body's kernel copy on the reader
+    thread, one TCP stream of ~10 GB/s keeps it ~0.9 busy at the N=1 rate
+    (profiles/r4): an SMT sibling busy decoding slowed it down. None when
+    fewer than ``min_cores`` physical cores would be left to the workers."""
+    if not rest:
+        return None
+    cores, seen = [], set()
+    for c in sorted(rest):
+        if c in seen:
+            continue
+        sib = core_siblings(c, root) & rest
+        seen |= sib | {c}
+        cores.append(sib or {c})
+    if len(cores) - 1 < min_cores:
+        return None
+    return set(cores[0]), set(rest) - cores[0]
+
+
 def loop_core_split(cpus: set, min_cores: int = 4, root: str = "") -> Optional[tuple]:
     """``(loop_cpus, other_cpus)`` for ``watcher.thread_pinning``: the lowest
     physical core of ``cpus`` (both hardware threads) for the event-loop

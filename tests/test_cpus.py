@@ -157,3 +157,17 @@ def test_eight_local_ranks_get_sane_shares(monkeypatch, own):
         assert 8 * (workers + 1) <= max(8, total), (mask, quota, workers)
         # spinning only with CPUs to spare
         assert cpus.auto_decode_spin_us() == (20.0 if share >= 8 else 0.0)
+
+
+def test_reader_core_split(tmp_path):
+    """thread_pinning auto: after the loop's core, the reader thread gets the
+    next physical core (both hardware threads), the decode workers the rest;
+    no reader core when fewer than 4 cores would be left to the workers."""
+    from k8s_watcher_amd.utils.cpus import loop_core_split, reader_core_split
+    for c in range(16):
+        write(tmp_path, f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list", "0-15")
+        write(tmp_path, f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list", f"{c % 8},{c % 8 + 8}")
+    _, rest = loop_core_split(set(range(16)), root=str(tmp_path))
+    reader, workers = reader_core_split(rest, root=str(tmp_path))
+    assert reader == {1, 9} and workers == set(range(2, 8)) | set(range(10, 16))
+    assert reader_core_split({1, 2, 3, 4, 9, 10, 11, 12}, root=str(tmp_path)) is None  # 3 cores left
