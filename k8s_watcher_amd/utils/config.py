@@ -540,9 +540,9 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
                                                   "clusterapi.pool.max_queued_bytes")),
             coalesce=_as_bool(pool.get("coalesce", False), "clusterapi.pool.coalesce"),
             native=_as_bool(pool.get("native", True), "clusterapi.pool.native"),
-            io_thread=(pool.get("io_thread") != "auto"
+            io_thread=(pool.get("io_thread", "auto") != "auto"
                        and _as_bool(pool.get("io_thread", False), "clusterapi.pool.io_thread")),
-            io_thread_auto=pool.get("io_thread") == "auto",
+            io_thread_auto=pool.get("io_thread", "auto") == "auto",
             io_thread_on_rate=_bounded_float(pool.get("io_thread_on_rate", 50000), "clusterapi.pool.io_thread_on_rate",
                                              1.0, 1e9),
             io_thread_off_rate=_bounded_float(pool.get("io_thread_off_rate", 5000),

@@ -95,19 +95,20 @@ def process_cpu_share(root: str = "") -> int:
 
 
 def auto_decode_threads(cpus: Optional[int] = None) -> int:
-    """Extra decode workers for one watch stream: leave a CPU for the event
-    loop thread and one for the notifier side, use at most 4 (the serial
-    apply phase caps the gain beyond that). With the reader hub framing the
-    bodies, the workers are the first on the event loop's side to touch each
-    line, and a fourth one cut the loop's wait for them by ~40%
-    (profiles/hub_framing_gpu_box.md).
+    """Decode workers (which also take the partitioned apply's partitions):
+    leave a CPU each for the event-loop thread, the reader thread and the
+    notifier's I/O thread, use at most 6. With the apply phase partitioned
+    over them (watcher.partitioned_apply) the serial stage no longer caps the
+    gain: six workers ran the cluster watch at 2.94-2.99M events/s on the
+    MI355X host's 16-CPU share (profiles/r4/io_thread); round 3's four had
+    cut the loop's wait for decode by ~40% (profiles/hub_framing_gpu_box.md).
 
     Without an explicit count, the CPUs are this process's share of the
     allowance when several shards run on the host: four ranks under one
     16-CPU quota asked for ~25 CPUs with 4 workers each and were throttled in
     123 of 134 scheduler periods (profiles/hub_framing_gpu_box.md)."""
     cpus = process_cpu_share() if cpus is None else cpus
-    return max(0, min(4, cpus - 2))
+    return max(0, min(6, cpus - 3))
 
 
 def auto_decode_spin_us(cpus: Optional[int] = None) -> float:

@@ -28,10 +28,11 @@ def test_cgroup_limits(tmp_path):
 
 def test_auto_decode_threads():
     assert cpus.auto_decode_threads(1) == 0
-    assert cpus.auto_decode_threads(2) == 0
-    assert cpus.auto_decode_threads(4) == 2
-    assert cpus.auto_decode_threads(5) == 3
-    assert cpus.auto_decode_threads(64) == 4
+    assert cpus.auto_decode_threads(3) == 0
+    assert cpus.auto_decode_threads(4) == 1
+    assert cpus.auto_decode_threads(8) == 5
+    assert cpus.auto_decode_threads(16) == 6
+    assert cpus.auto_decode_threads(64) == 6
 
 
 def test_parse_cpu_list():
@@ -79,14 +80,14 @@ def test_auto_decode_threads_per_local_process(monkeypatch):
     # the 1-GPU box: pinned to a 16-CPU domain under a 16-CPU job quota
     monkeypatch.setattr(cpus.os, "sched_getaffinity", lambda pid: set(range(16)))
     monkeypatch.setattr(cpus, "cgroup_cpu_limit", lambda root="": 16.0)
-    assert cpus.auto_decode_threads() == 4
+    assert cpus.auto_decode_threads() == 6
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
-    assert cpus.process_cpu_share() == 4 and cpus.auto_decode_threads() == 2
+    assert cpus.process_cpu_share() == 4 and cpus.auto_decode_threads() == 1
     # a whole node without a quota: a shard pinned to its own domain keeps it
     monkeypatch.setattr(cpus, "cgroup_cpu_limit", lambda root="": None)
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
     monkeypatch.setenv(cpus.OWN_CPUS_ENV, "1")
-    assert cpus.process_cpu_share() == 16 and cpus.auto_decode_threads() == 4
+    assert cpus.process_cpu_share() == 16 and cpus.auto_decode_threads() == 6
     monkeypatch.delenv(cpus.OWN_CPUS_ENV)
     # ... an unpinned one shares the host's CPUs
     monkeypatch.setattr(cpus.os, "sched_getaffinity", lambda pid: set(range(256)))
@@ -118,7 +119,7 @@ def test_cpuset_container_splits_the_mask_between_local_shards(monkeypatch):
     monkeypatch.setattr(cpus, "cgroup_cpu_limit", lambda root="": None)
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
     assert cpus.process_cpu_share() == 4
-    assert cpus.auto_decode_threads() == 2 and cpus.auto_decode_spin_us() == 0.0
+    assert cpus.auto_decode_threads() == 1 and cpus.auto_decode_spin_us() == 0.0
     monkeypatch.setenv(cpus.OWN_CPUS_ENV, "1")  # the launcher pinned each shard to its own 16
     assert cpus.process_cpu_share() == 16 and cpus.auto_decode_spin_us() == 20.0
 
@@ -154,7 +155,7 @@ def test_eight_local_ranks_get_sane_shares(monkeypatch, own):
         total = quota if quota is not None else len(mask)
         assert 1 <= share <= max(1, total // 8), (mask, quota, share)
         workers = cpus.auto_decode_threads()
-        assert 8 * (workers + 1) <= max(8, total), (mask, quota, workers)
+        assert 8 * (workers + 3) <= max(24, total), (mask, quota, workers)  # + loop, reader, notifier I/O
         # spinning only with CPUs to spare
         assert cpus.auto_decode_spin_us() == (20.0 if share >= 8 else 0.0)
 

@@ -424,11 +424,12 @@ def test_io_thread_auto_switches_both_ways_without_loss():
         for burst in range(3):
             t_end = time.monotonic() + 0.6
             k = 0
-            while time.monotonic() < t_end:  # ~2,000/s for 0.6 s
-                uid = f"u{k % 50}"
-                pool.submit(uid, "MODIFIED", "default", f"b{burst}-{k}", core(uid, name=f"b{burst}-{k}"), 0, TS)
-                sent.append((uid, f"b{burst}-{k}"))
-                k += 1
+            while time.monotonic() < t_end:  # >= 2,000/s for 0.6 s, even on a loaded machine (3 per turn)
+                for _ in range(3):
+                    uid = f"u{k % 50}"
+                    pool.submit(uid, "MODIFIED", "default", f"b{burst}-{k}", core(uid, name=f"b{burst}-{k}"), 0, TS)
+                    sent.append((uid, f"b{burst}-{k}"))
+                    k += 1
                 pool.flush()
                 await asyncio.sleep(0.0005)
             modes.append(pool.threaded)
@@ -465,9 +466,10 @@ def test_io_thread_auto_hands_back_with_requests_in_flight():
         pool = NativeNotifierPool(s, m)
         n = 0
         t_end = time.monotonic() + 0.5
-        while time.monotonic() < t_end:
-            pool.submit(f"u{n}", "ADDED", "default", f"p{n}", core(f"u{n}"), 0, TS)
-            n += 1
+        while time.monotonic() < t_end:  # well above io_thread_on_rate even on a loaded machine
+            for _ in range(3):
+                pool.submit(f"u{n}", "ADDED", "default", f"p{n}", core(f"u{n}"), 0, TS)
+                n += 1
             pool.flush()
             await asyncio.sleep(0.001)
         was_threaded = pool.threaded
