@@ -783,8 +783,9 @@ class WatcherService:
         ``watcher.malloc_trim_min_free_mb`` free, and every trim is timed
         (``malloc_trim_last_ms`` / ``malloc_trim_max_ms`` gauges,
         ``malloc_trim_us`` counter) so a latency outlier can be checked
-        against it. Under sustained load it waits
-        for a quiet moment (the freed pages would be reused at once anyway)."""
+        against it. It waits for half a second
+        without events (up to nine periods; then it trims anyway), so a trim
+        does not stall notifications in flight."""
         from ..ops.native import load
         kw = load()
         trim, info = kw.malloc_trim, kw.malloc_info
@@ -801,26 +802,30 @@ class WatcherService:
             return time.perf_counter() - t
 
         async def quiet_moment() -> bool:
-            # a trim under load makes every allocating thread wait on its
-            # arena (12.8 ms once on the MI355X host right after the
-            # saturated headline) and the pages come straight back: wait,
-            # up to one period, for a quarter second with little traffic
+            # a trim makes every allocating thread wait on its arena while it
+            # walks it (7.5-15 ms on the MI355X host with the heap the
+            # saturated bench leaves): a notification in flight then waits
+            # too. Wait, up to one period, for half a second with no event.
             deadline = time.monotonic() + period
             while time.monotonic() < deadline:
                 n0 = c["events_received"]
-                await asyncio.sleep(0.25)
-                if c["events_received"] - n0 <= 250:  # under ~1k events/s
+                await asyncio.sleep(0.5)
+                if c["events_received"] == n0:
                     return True
             return False
 
+        deferred = 0
         while True:
             await asyncio.sleep(period)
             if min_free > 0 and info()["free_bytes"] < min_free:
                 c["malloc_trims_skipped"] += 1
                 continue
-            if not await quiet_moment():
+            # a watcher that is never quiet still trims, every tenth period
+            if deferred < 9 and not await quiet_moment():
+                deferred += 1
                 c["malloc_trims_deferred"] += 1
                 continue
+            deferred = 0
             try:
                 secs = await loop.run_in_executor(None, timed_trim)
             except RuntimeError as exc:  # the executor is going away (shutdown)

@@ -56,7 +56,7 @@ COUNTERS = (
     "checkpoints_written",
     "malloc_trims",         # times the C heap's free pages were handed back (watcher.malloc_trim_seconds)
     "malloc_trims_skipped",  # ... periods with less free heap than watcher.malloc_trim_min_free_mb (no trim)
-    "malloc_trims_deferred",  # ... periods under sustained load (no quiet quarter second): trimmed later
+    "malloc_trims_deferred",  # ... periods without a quiet half second (trimmed later; at the latest every 10th)
     "malloc_trim_us",       # time spent in those trims (every arena locked meanwhile), microseconds
     "checkpoint_owed_resent",  # owed notifications a format-2 checkpoint re-submitted on start
     "namespace_changes",    # namespace set changes seen by watcher.namespace_scope: discover

@@ -48,7 +48,7 @@ def test_service_trims_periodically():
     async def body():
         stub = _trim_stub(0.0)
         task = asyncio.ensure_future(WatcherService._malloc_trim_loop(stub, 0.01))
-        await asyncio.sleep(0.8)  # each trim waits for a quiet quarter second first
+        await asyncio.sleep(1.4)  # each trim waits for a quiet half second first
         task.cancel()
         return stub.metrics
 
@@ -81,7 +81,7 @@ def test_service_defers_trim_under_load():
     async def body():
         stub = _trim_stub(0.0)
         task = asyncio.ensure_future(WatcherService._malloc_trim_loop(stub, 0.05))
-        t_end = asyncio.get_running_loop().time() + 0.9
+        t_end = asyncio.get_running_loop().time() + 1.2
         while asyncio.get_running_loop().time() < t_end:  # ~20k events/s
             stub.metrics.c["events_received"] += 100
             await asyncio.sleep(0.005)
