@@ -700,12 +700,17 @@ async def rank_main(args, d: Dist) -> dict:
         metrics.latency.reset()
         k_lat = (args.warmup + args.steps) * R
         lat = []
+        lat_seconds: list = []
+        lat_io = None
         if args.latency_seconds > 0:
             count = max(1, int(args.latency_rate * d.world * args.latency_seconds))
             count = min(count, shared["events_per_step"])
+            io_before = getattr(svc.notifier, "threaded", None)
             await run_latency(fx, d, svc, c, k_lat, args.latency_rate * d.world, count, args.step_timeout,
-                              notifiable)
+                              notifiable, seconds_out=lat_seconds, metrics=metrics)
             lat = list(metrics.latency.samples or [])
+            lat_io = {"threaded_at_start": io_before, "threaded_at_end": getattr(svc.notifier, "threaded", None),
+                      "io_switches": c.get("notify_io_switches", 0)}
         # and at 10x that, long enough for >= 5,000 notified samples in the 20%-notifying profile
         lat_hi = []
         lat_hi_seconds: list = []
@@ -738,7 +743,8 @@ async def rank_main(args, d: Dist) -> dict:
                 # the reference's bench runs do: no figure against an https one)
                 ref = await run_reference(args, fx, shared, targets, k_lat + 1)
         return {"elapsed": elapsed, "events": events, "notified": notified, "series": series, "rss_mib": rss,
-                "timed_seconds": timed_seconds, "lat_hi_seconds": lat_hi_seconds,
+                "timed_seconds": timed_seconds, "lat_hi_seconds": lat_hi_seconds, "lat_seconds": lat_seconds,
+                "lat_io": lat_io,
                 "trims": {"count": c.get("malloc_trims", 0), "skipped": c.get("malloc_trims_skipped", 0),
                           "total_ms": round(c.get("malloc_trim_us", 0) / 1e3, 2),
                           "max_ms": round(metrics.gauges["malloc_trim_max_ms"](), 2)
@@ -1304,6 +1310,9 @@ def main(argv=None) -> int:
         # rank 0, per second of the timed steps / the 1k ev/s latency phase: what else happened
         # in the seconds the rate dipped or a notification took > 1 ms (SecondSeries)
         "rate_dips_rank0": explain_seconds(res["timed_seconds"]),
+        "latency_seconds_rank0": {"rows": res["lat_seconds"], "notifier_io": res["lat_io"],
+                                  "seconds_over_1ms": [dict(r, second=i) for i, r in enumerate(res["lat_seconds"])
+                                                       if r.get("lat_over_1ms")]},
         "latency_high_seconds_rank0": {"rows": res["lat_hi_seconds"],
                                        "seconds_over_1ms": [dict(r, second=i) for i, r in
                                                             enumerate(res["lat_hi_seconds"])
