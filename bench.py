@@ -639,6 +639,7 @@ async def rank_main(args, d: Dist) -> dict:
 
         for k in range(args.warmup):
             await run_step(k, per_step)
+        getattr(svc.notifier, "flush", lambda: None)()  # the warm-up's samples the I/O thread still holds
         metrics.latency.reset()
         d.barrier()
         if args.soak_minutes > 0:
@@ -694,6 +695,17 @@ async def rank_main(args, d: Dist) -> dict:
             probe["loop_cpu_ns"] = int((cpu1["thread_loop"] - cpu0["thread_loop"]) * 1e9)
         events = c["events_received"] - n0
         notified = c["notify_delivered"] - s0
+
+        def settle_samples() -> None:
+            # the notifier's I/O thread hands latency samples over in blocks of
+            # 4,096: take what it still holds now, so the samples of one phase
+            # do not land in the next (they had put the saturated phase's tail
+            # into the 100 ev/s p50 whenever a phase began with the thread on)
+            flush = getattr(svc.notifier, "flush", None)
+            if flush is not None:
+                flush()
+
+        settle_samples()
         sat = list(metrics.latency.samples or [])
 
         # latency at the nominal rate, per rank (untimed)
@@ -708,6 +720,7 @@ async def rank_main(args, d: Dist) -> dict:
             io_before = getattr(svc.notifier, "threaded", None)
             await run_latency(fx, d, svc, c, k_lat, args.latency_rate * d.world, count, args.step_timeout,
                               notifiable, seconds_out=lat_seconds, metrics=metrics)
+            settle_samples()
             lat = list(metrics.latency.samples or [])
             lat_io = {"threaded_at_start": io_before, "threaded_at_end": getattr(svc.notifier, "threaded", None),
                       "io_switches": c.get("notify_io_switches", 0)}
@@ -717,12 +730,14 @@ async def rank_main(args, d: Dist) -> dict:
         cg_hi = None
         if args.latency_rate_high > 0 and args.latency_seconds_high > 0:
             cg_a = cgroup_cpu()
+            settle_samples()
             metrics.latency.reset()
             k_lat += 1
             count = max(1, int(args.latency_rate_high * d.world * args.latency_seconds_high))
             count = min(count, shared["events_per_step"])
             await run_latency(fx, d, svc, c, k_lat, args.latency_rate_high * d.world, count, args.step_timeout,
                               notifiable, seconds_out=lat_hi_seconds, metrics=metrics)
+            settle_samples()
             lat_hi = list(metrics.latency.samples or [])
             cg_hi = cgroup_delta(cg_a, cgroup_cpu())
         failed = c["notify_failed"]
