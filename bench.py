@@ -110,6 +110,7 @@ def parse_args(argv=None):
     ap.add_argument("--watch-reader", default=None, choices=["native", "asyncio"], help="watcher.watch_reader")
     ap.add_argument("--watch-reader-buffers", type=int, default=None, help="watcher.watch_reader_buffers")
     ap.add_argument("--watch-reader-max-bytes", type=int, default=None, help="watcher.watch_reader_max_bytes")
+    ap.add_argument("--recv-slice", type=int, default=None, help="watcher.watch_recv_slice (bytes per recv, framed in L2)")
     ap.add_argument("--thread-pinning", default=None, choices=["auto", "loop", "none"], help="watcher.thread_pinning")
     ap.add_argument("--no-placement", dest="placement", action="store_false",
                     help="no per-rank L3 domain assignment (each watcher still pins per watcher.decode_affinity)")
@@ -480,6 +481,7 @@ async def rank_main(args, d: Dist) -> dict:
                         **({"watch_reader_buffers": args.watch_reader_buffers} if args.watch_reader_buffers else {}),
                         **({"watch_reader_max_bytes": args.watch_reader_max_bytes}
                            if args.watch_reader_max_bytes is not None else {}),
+                        **({"watch_recv_slice": args.recv_slice} if args.recv_slice is not None else {}),
                         **({"thread_pinning": args.thread_pinning} if args.thread_pinning else {}),
                         **({"validate": args.validate} if args.validate else {}),
                         **({"hub_dispatch": args.hub_dispatch == "on"} if args.hub_dispatch else {}),
@@ -657,6 +659,8 @@ async def rank_main(args, d: Dist) -> dict:
         dpool = svc._decode_pool or None
         pool0 = dpool.stats() if dpool is not None else None
         gc_stats = _GcStats()  # collector pauses on the loop thread over the timed steps
+        hub = getattr(svc, "_reader_hub", None)
+        hub0 = hub.stats() if hub is not None else None
         cpu0 = cpu_snapshot(fx)
         cg0 = cgroup_cpu()
         t0 = time.perf_counter()
@@ -678,6 +682,13 @@ async def rank_main(args, d: Dist) -> dict:
             prof.dump_stats(os.environ["BENCH_PROFILE"])
         cpu1 = cpu_snapshot(fx)
         cg_timed = cgroup_delta(cg0, cgroup_cpu())
+        reader_timed = None
+        if hub0 is not None:  # the reader thread over the timed steps: in recv (the copy) vs framing
+            hub1 = hub.stats()
+            dr, df, db = (hub1[k] - hub0[k] for k in ("recv_ns", "frame_ns", "recv_bytes"))
+            reader_timed = {"recv_frac": round(dr / 1e9 / elapsed, 3), "frame_frac": round(df / 1e9 / elapsed, 3),
+                            "recv_gb_per_s": round(db / dr, 2) if dr else None,
+                            "bytes_per_event": round(db / max(1, c["events_received"] - n0))}
         zc = None
         if d.rank == 0:  # the replay fixture's zero-copy sends (bytes, slot waits) so far
             reply = await fx.cmd("ZCSTATS")
@@ -742,9 +753,9 @@ async def rank_main(args, d: Dist) -> dict:
             cg_hi = cgroup_delta(cg_a, cgroup_cpu())
         failed = c["notify_failed"]
         delivered_total = c["notify_delivered"]
-        hub = getattr(svc, "_reader_hub", None)
         reader = dict(hub.stats(), mode="native") if hub is not None else {"mode": "asyncio"}
         reader["hub_dispatch_watches"] = c["watches_hub_dispatch"]
+        reader["timed"] = reader_timed
         svc.stop()
         await svc.shutdown()
         d.barrier()  # every shard stopped: the sink's counts are final

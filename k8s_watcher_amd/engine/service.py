@@ -295,7 +295,8 @@ class WatcherService:
                 self._reader_hub = WatchReaderHub(s.watcher.watch_read_bytes or (4 << 20),
                                                   s.watcher.watch_reader_buffers,
                                                   max_bytes=s.watcher.watch_reader_max_bytes,
-                                                  frame=s.watcher.hub_framing)
+                                                  frame=s.watcher.hub_framing,
+                                                  recv_slice=s.watcher.watch_recv_slice)
                 self.api.http.reader_hub = self._reader_hub
                 hub = self._reader_hub
                 self.metrics.gauges["watch_reader_streams"] = lambda: float(len(hub.protos))

@@ -565,13 +565,16 @@ def test_busy_streams_grow_only_to_their_share_of_the_pool():
         b.close()
 
 
+@pytest.mark.parametrize("recv_slice", [0, 4096, 5000])
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_hub_framing_matches_pipeline_framing_on_random_chunking(seed):
+def test_hub_framing_matches_pipeline_framing_on_random_chunking(seed, recv_slice):
     """Once a chunked body is bound, the hub frames it (chunk de-framing and
     line splitting on its reader thread, HubFramer) and the pipeline walks
     line items: random chunk sizes, random send pieces and small buffers put
     chunk headers, line ends and buffer ends everywhere — the result is
-    identical to the pipeline framing the same bytes itself."""
+    identical to the pipeline framing the same bytes itself. With a recv
+    slice (watcher.watch_recv_slice) each recv() of a buffer is framed on its
+    own, so slice ends land everywhere too."""
     import random
     import threading
     from test_native_pipeline import Recorder, run_native, stream
@@ -597,6 +600,8 @@ def test_hub_framing_matches_pipeline_framing_on_random_chunking(seed):
     p.attach_native(load().DecodePool(2))
     p.sync_native_log()
     core = load().ReaderHub(16 * 1024, 16)
+    core.set_recv_slice(recv_slice)
+    assert core.stats()["recv_slice"] == recv_slice
     a, b = socket.socketpair()
     sid = core.add(os.dup(b.fileno()))
     core.bind(sid, p.native, True)
@@ -629,10 +634,26 @@ def test_hub_framing_matches_pipeline_framing_on_random_chunking(seed):
     assert {u: list(e) for u, e in p.cache.items()} == {u: list(e) for u, e in want_cache.items()}
     assert ctrl == want_ctrl
     assert p.native.last_rv() == want_rv and p.native.body_done()
-    assert core.stats()["framed_reads"] > 0  # the hub did frame (after the first take)
+    st = core.stats()
+    assert st["framed_reads"] > 0 and st["frame_ns"] > 0  # the hub did frame (after the first take)
+    assert st["recv_bytes"] == len(raw) and st["recv_ns"] > 0
     core.close()
     a.close()
     b.close()
+
+
+def test_recv_slice_setting():
+    from k8s_watcher_amd.utils.config import ConfigError, load_settings
+    assert load_settings("production", environ={}).watcher.watch_recv_slice == 0
+    s = load_settings("production", overrides={"watcher": {"watch_recv_slice": 262144}}, environ={})
+    assert s.watcher.watch_recv_slice == 262144
+    for bad in (-1, 100):
+        with pytest.raises(ConfigError):
+            load_settings("production", overrides={"watcher": {"watch_recv_slice": bad}}, environ={})
+    core = load().ReaderHub(16 * 1024, 4)
+    with pytest.raises(ValueError):
+        core.set_recv_slice(100)
+    core.close()
 
 
 def test_hub_framing_reports_bad_chunk_size_like_the_pipeline():
