@@ -36,7 +36,7 @@ from ..ops import native
 class WatchReaderHub:
     def __init__(self, buf_bytes: int, nbufs: int = 64,
                  loop: Optional[asyncio.AbstractEventLoop] = None, max_bytes: int = 0, frame: bool = True,
-                 recv_slice: int = 0) -> None:
+                 recv_slice: int = 0, depth: int = 2) -> None:
         self.loop = loop or asyncio.get_running_loop()
         # max_bytes: read-ahead over all streams (0: the whole pool); frame: the
         # hub's thread de-chunks and splits bound bodies (watcher.hub_framing)
@@ -46,6 +46,9 @@ class WatchReaderHub:
         # L2 (watcher.watch_recv_slice; 0: one recv per buffer)
         if recv_slice:
             self.core.set_recv_slice(int(recv_slice))
+        # depth: buffers read ahead per stream (watcher.watch_reader_depth)
+        if depth != 2:
+            self.core.set_depth(int(depth))
         self.protos: Dict[int, object] = {}
         self._tls: Dict[tuple, object] = {}
         self._flush: Dict[object, object] = {}  # bind(): once per dispatch

@@ -203,12 +203,14 @@ def test_tls_streams_stay_on_asyncio():
     assert run(body()) is False
 
 
-def test_read_ahead_is_capped_per_stream():
-    """However large the pool, one stream gets at most two buffers ahead of
-    the consumer: a slow event loop leaves the backlog in the socket (TCP flow
-    control), not in user memory."""
+@pytest.mark.parametrize("depth", [2, 4])
+def test_read_ahead_is_capped_per_stream(depth):
+    """However large the pool, one stream gets at most two buffers (or
+    watcher.watch_reader_depth) ahead of the consumer: a slow event loop
+    leaves the backlog in the socket (TCP flow control), not in user memory."""
     mod = load()
     core = mod.ReaderHub(4096, 16)
+    core.set_depth(depth)
     a, b = socket.socketpair()
     sid = core.add(os.dup(b.fileno()))
     data = os.urandom(400_000)
@@ -220,7 +222,7 @@ def test_read_ahead_is_capped_per_stream():
     for _ in range(20):
         held += [(buf, bytes(view)) for _s, buf, view, _ns, _e in core.take() if view is not None]
         time.sleep(0.01)
-    assert 1 <= len(held) <= 2
+    assert (1 if depth == 2 else 3) <= len(held) <= depth
     out = bytearray(b"".join(x for _, x in held))
     for buf, _ in held:
         core.release(buf)
@@ -650,9 +652,17 @@ def test_recv_slice_setting():
     for bad in (-1, 100):
         with pytest.raises(ConfigError):
             load_settings("production", overrides={"watcher": {"watch_recv_slice": bad}}, environ={})
+    assert load_settings("production", environ={}).watcher.watch_reader_depth == 2
+    for bad in (1, 9):
+        with pytest.raises(ConfigError):
+            load_settings("production", overrides={"watcher": {"watch_reader_depth": bad}}, environ={})
     core = load().ReaderHub(16 * 1024, 4)
     with pytest.raises(ValueError):
         core.set_recv_slice(100)
+    with pytest.raises(ValueError):
+        core.set_depth(9)
+    core.set_depth(4)
+    assert core.stats()["depth"] == 4
     core.close()
 
 
