@@ -342,8 +342,12 @@ class WatcherService:
             self.log.info(f"Monitoring namespaces: {s.watcher.namespaces}")
         else:
             self.log.info("Monitoring all namespaces")
-        for ns in scopes:
+        for i, ns in enumerate(scopes):
             self._start_scope(ns, primed=bool(saved_rvs))
+            if i % 64 == 63:  # a thousand namespaces: let the started scopes (and the loop) run meanwhile
+                await asyncio.sleep(0)
+                if self._stop.is_set():
+                    break
         if s.metrics.enabled and self.serve_metrics:
             self._metrics_server = await start_metrics_server(self.metrics, s.metrics.host, s.metrics.port,
                                                               debug=s.metrics.debug)
