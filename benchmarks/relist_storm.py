@@ -177,9 +177,6 @@ async def main_async(args) -> dict:
         lag.start()
         cpu0, t0 = os.times(), time.perf_counter()
         await asyncio.wait_for(svc.start(), args.timeout)
-        start_s = time.perf_counter() - t0
-        start_lag = lag.stop()  # the service's start: extension, pools, namespace discovery, the reflectors' tasks
-        lag.start()
         scopes = len(svc.reflectors)
         await wait_quiet(svc, c, scopes, args.timeout)
         initial_s = time.perf_counter() - t0
@@ -239,7 +236,6 @@ async def main_async(args) -> dict:
                        "initial_sync": args.initial_sync},
             "fixture_setup_s": round(fixture_s, 2),
             "initial": {"wall_s": round(initial_s, 3), "watcher_cpu_s": cpu(cpu0, cpu1), "loop_lag": initial_lag,
-                        "start_s": round(start_s, 3), "start_loop_lag": start_lag,
                         "relist": slices(initial_slices), "exactly_once": initial_ok, "notified": len(keys0)},
             "storm": {"expired_watches": expired["expired"], "wall_s": round(storm_s, 3),
                       "watcher_cpu_s": cpu(cpu2, cpu3), "loop_lag": storm_lag, "relist": slices(storm),
