@@ -242,8 +242,10 @@ class _VerifyingState(SinkState):
         self.keys[k] = self.keys.get(k, 0) + 1
 
 
-def _native_sink(port: int, verify: bool):
-    """A ``_kwcore.SinkServer`` on a SO_REUSEPORT socket bound to ``port``."""
+def _native_sink(port: int, verify: bool, reserve: int = 0):
+    """A ``_kwcore.SinkServer`` on a SO_REUSEPORT socket bound to ``port``
+    (``reserve``: distinct keys expected in verify mode; the table is sized
+    for them instead of rehashing while it serves)."""
     from ..ops.native import load
     sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
     sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
@@ -251,14 +253,14 @@ def _native_sink(port: int, verify: bool):
     sock.bind(("127.0.0.1", port))
     sock.listen(1024)
     try:
-        return load().SinkServer(sock.fileno(), b"/api/pods/update", verify)  # serves a dup of the socket
+        return load().SinkServer(sock.fileno(), b"/api/pods/update", verify, reserve)  # serves a dup of the socket
     finally:
         sock.close()
 
 
 def run_sink_process(port: int, workers: int = 1, latency: float = 0.0,
                      verify_dir: Optional[str] = None, tls: Optional[Tuple[str, str]] = None,
-                     engine: str = "auto") -> None:
+                     engine: str = "auto", expect_keys: int = 0) -> None:
     """Blocking: serve on ``port`` with ``workers`` SO_REUSEPORT processes (bench helper).
 
     With ``verify_dir`` every worker records ``uid|event_type|phase`` counts and
@@ -285,7 +287,7 @@ def run_sink_process(port: int, workers: int = 1, latency: float = 0.0,
         pids.append(pid)
 
     async def serve_native() -> None:
-        srv = _native_sink(port, bool(verify_dir))
+        srv = _native_sink(port, bool(verify_dir), expect_keys)
         stop = asyncio.Event()
         loop = asyncio.get_running_loop()
 
@@ -351,6 +353,8 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--workers", type=int, default=1)
     ap.add_argument("--latency", type=float, default=0.0)
     ap.add_argument("--verify-dir", default=None, help="record payload keys, dump on SIGTERM")
+    ap.add_argument("--expect-keys", type=int, default=0,
+                    help="native sink, verify mode: distinct keys per worker to size the key table for")
     ap.add_argument("--tls-cert", default=None, help="serve https with this certificate (and --tls-key)")
     ap.add_argument("--tls-key", default=None)
     ap.add_argument("--engine", default="auto", choices=["auto", "native", "python"],
@@ -358,7 +362,7 @@ def main(argv: Optional[List[str]] = None) -> None:
     args = ap.parse_args(argv)
     tls = (args.tls_cert, args.tls_key) if args.tls_cert else None
     print(f"stub clusterapi listening on {'https' if tls else 'http'}://127.0.0.1:{args.port}", flush=True)
-    run_sink_process(args.port, args.workers, args.latency, args.verify_dir, tls, args.engine)
+    run_sink_process(args.port, args.workers, args.latency, args.verify_dir, tls, args.engine, args.expect_keys)
 
 
 if __name__ == "__main__":

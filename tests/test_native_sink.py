@@ -56,9 +56,11 @@ BODIES = [
 ]
 
 
-def test_native_sink_pipelined_answers_and_keys():
+@pytest.mark.parametrize("reserve", [0, 4096])
+def test_native_sink_pipelined_answers_and_keys(reserve):
+    """reserve: the key table sized up front (bench --expect-keys), also after a reset."""
     port = _free_port()
-    srv = _native_sink(port, True)
+    srv = _native_sink(port, True, reserve)
     try:
         with socket.create_connection(("127.0.0.1", port)) as s:
             reqs = [_post(b) for b in BODIES] + [
@@ -149,3 +151,5 @@ def test_sink_process_native_verify_dump(tmp_path):
 def test_native_sink_rejects_bad_fd():
     with pytest.raises(OSError):
         load().SinkServer(-1)
+    with pytest.raises(ValueError):
+        load().SinkServer(0, b"/api/pods/update", True, -1)
