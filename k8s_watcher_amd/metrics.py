@@ -222,13 +222,19 @@ def memory_census(top: int = 40) -> Dict[str, object]:
     import gc
     import sys
     import tracemalloc
+    # live objects only: without a collection first the counts include cyclic
+    # garbage the collector has not reached yet (a closed connection's
+    # transport <-> protocol cycle waits for a gen-2 pass: 23 "extra"
+    # transports in a soak's census diff were exactly that)
+    collected = gc.collect()
     counts: Dict[str, int] = {}
     for o in gc.get_objects():
         t = type(o)
         k = f"{t.__module__}.{t.__qualname__}"
         counts[k] = counts.get(k, 0) + 1
     out: Dict[str, object] = {
-        "gc_objects": sum(counts.values()), "allocated_blocks": sys.getallocatedblocks(),
+        "gc_objects": sum(counts.values()), "garbage_collected": collected,
+        "allocated_blocks": sys.getallocatedblocks(),
         "types": dict(sorted(counts.items(), key=lambda kv: -kv[1])[:top]), "gc_counts": list(gc.get_count())}
     if tracemalloc.is_tracing():
         snap = tracemalloc.take_snapshot().filter_traces(

@@ -174,4 +174,5 @@ def test_debug_memory_endpoint_only_when_enabled():
         tracemalloc.stop()
     assert s0 == 404 and s1 == 200
     assert doc["gc_objects"] > 1000 and "builtins.dict" in doc["types"]
+    assert doc["garbage_collected"] >= 0  # counted after a collection: live objects only
     assert doc["tracemalloc"]["traced_bytes"] > 0 and doc["tracemalloc"]["top"]
