@@ -65,7 +65,8 @@ def test_reader_hub_on_host():
     test_reader_hub.test_hub_pause_stops_reading_and_remove_closes()
     test_reader_hub.test_pool_exhaustion_is_backpressure_not_loss()
     test_reader_hub.test_http_stream_adopted_by_hub_end_to_end()
-    test_reader_hub.test_read_ahead_is_capped_per_stream()
+    for depth in (2, 4):
+        test_reader_hub.test_read_ahead_is_capped_per_stream(depth)
     test_reader_hub.test_read_ahead_is_capped_in_bytes_over_all_streams()
     # the thread recv()s outside its lock: takes and removals racing it, on the host's cores
     test_reader_hub.test_take_and_remove_race_the_reader_thread()
@@ -79,7 +80,8 @@ def test_hub_framing_and_grouped_dispatch_on_host():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import test_reader_hub
     for seed in (1, 2, 3):
-        test_reader_hub.test_hub_framing_matches_pipeline_framing_on_random_chunking(seed)
+        for recv_slice in (0, 4096, 5000):
+            test_reader_hub.test_hub_framing_matches_pipeline_framing_on_random_chunking(seed, recv_slice)
     test_reader_hub.test_take_dispatch_groups_many_bound_streams_like_serial_feeding()
     test_reader_hub.test_busy_streams_grow_only_to_their_share_of_the_pool()
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
@@ -99,7 +101,8 @@ def test_native_sink_on_host(tmp_path):
     the SO_REUSEPORT worker processes' dumps, on the host."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import test_native_sink
-    test_native_sink.test_native_sink_pipelined_answers_and_keys()
+    for reserve in (0, 4096):
+        test_native_sink.test_native_sink_pipelined_answers_and_keys(reserve)
     test_native_sink.test_native_sink_many_connections()
     test_native_sink.test_sink_process_native_verify_dump(tmp_path)
 
