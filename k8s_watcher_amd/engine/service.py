@@ -26,6 +26,7 @@ all-namespaces watch: reflectors start and stop as namespaces come and go.
 from __future__ import annotations
 
 import asyncio
+import gc
 import logging
 import os
 import time
@@ -94,6 +95,7 @@ class WatcherService:
         self.notifier = None
         self.pipeline: Optional[EventPipeline] = None
         self._decode_pool = None
+        self._gc_frozen = False
         self._reader_hub = None
         self.thread_placement = None
         self._loop_affinity = None
@@ -359,6 +361,10 @@ class WatcherService:
         if self.ns_watcher is not None:
             self._on_namespaces(self.ns_watcher.names)  # changes seen while the first scopes started
         await self._wait_synced()
+        if s.watcher.gc_freeze and not self._stop.is_set():
+            gc.collect()
+            gc.freeze()
+            self._gc_frozen = True
         self.metrics.ready = True
         self.started.set()
 
@@ -634,6 +640,9 @@ class WatcherService:
         overwrite newer state.
         """
         self.log.info("Stopping Pod watcher...")
+        if self._gc_frozen:  # this service's objects are collectable again (a leader's next term)
+            self._gc_frozen = False
+            gc.unfreeze()
         if self.ns_watcher is not None:
             self.ns_watcher.stop()
         for r in self.reflectors:

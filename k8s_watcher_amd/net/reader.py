@@ -34,6 +34,8 @@ from ..ops import native
 
 
 class WatchReaderHub:
+    DISPATCH_SLICE_S = 0.004  # longest delivery of hub reads in one loop turn
+
     def __init__(self, buf_bytes: int, nbufs: int = 64,
                  loop: Optional[asyncio.AbstractEventLoop] = None, max_bytes: int = 0, frame: bool = True,
                  recv_slice: int = 0, depth: int = 2) -> None:
@@ -52,6 +54,7 @@ class WatchReaderHub:
         self.protos: Dict[int, object] = {}
         self._tls: Dict[tuple, object] = {}
         self._flush: Dict[object, object] = {}  # bind(): once per dispatch
+        self._pending = None  # (items, touched) a dispatch's delivery left for the next turn
         self._fd = self.core.fileno()
         self.loop.add_reader(self._fd, self._on_ready)
         self.closed = False
@@ -122,18 +125,23 @@ class WatchReaderHub:
 
     def _on_ready(self) -> None:
         core = self.core
-        items, touched = core.take_dispatch()
-        protos = self.protos
-        if touched:
-            now = time.monotonic()
-            for sid in touched:
-                proto = protos.get(sid)
-                if proto is not None:
-                    proto.last_activity = now
+        if self._pending is not None:  # the rest of the last dispatch first: no newer read may pass it
+            items, touched = self._pending
+            self._pending = None
+        else:
+            items, touched = core.take_dispatch()
+            protos = self.protos
+            if touched:
+                now = time.monotonic()
+                for sid in touched:
+                    proto = protos.get(sid)
+                    if proto is not None:
+                        proto.last_activity = now
         try:
-            self._deliver(core, items)
+            self._deliver(core, items, touched)
         finally:
             if touched:
+                protos = self.protos
                 for sid in touched:
                     proto = protos.get(sid)
                     sync = getattr(proto, "hub_sync", None) if proto is not None else None
@@ -142,28 +150,43 @@ class WatchReaderHub:
                 for flush in list(self._flush.values()):
                     flush()
 
-    def _deliver(self, core, items) -> None:
-        for sid, buf, view, read_ns, err in items:
+    def _deliver(self, core, items, touched=()) -> None:
+        # one loop turn delivers for at most DISPATCH_SLICE_S: a storm hands the
+        # loop hundreds of reads that need Python at once (every watch of a
+        # 1,000-namespace cluster answering 410 together: ~50 us each); the rest
+        # waits for the next turn, ahead of anything newer (take_dispatch is not
+        # called while a rest is pending, so a bound stream's later reads stay
+        # queued behind its attention read)
+        deadline = time.perf_counter() + self.DISPATCH_SLICE_S
+        last = len(items) - 1
+        for i, (sid, buf, view, read_ns, err) in enumerate(items):
             if buf == -2:  # a bound stream's read that needs Python (take_dispatch)
                 proto = self.protos.get(sid)
                 if proto is not None:
                     proto.hub_native(view, read_ns, bool(err))
-                continue
-            try:
-                proto = self.protos.get(sid)
-                if proto is not None:
-                    if view is not None:
-                        proto.hub_data(view, read_ns)
-                    else:
-                        proto.hub_eof(err)
-            finally:
+            else:
+                self._deliver_read(core, sid, buf, view, read_ns, err)
+            if i < last and not self.closed and time.perf_counter() > deadline:
+                self._pending = (items[i + 1:], touched)
+                self.loop.call_soon(self._on_ready)
+                return
+
+    def _deliver_read(self, core, sid, buf, view, read_ns, err) -> None:
+        try:
+            proto = self.protos.get(sid)
+            if proto is not None:
                 if view is not None:
-                    try:
-                        view.release()
-                    except BufferError:  # a consumer kept a slice: never reuse under it
-                        continue
-                if buf >= 0 and not self.closed:
-                    core.release(buf)
+                    proto.hub_data(view, read_ns)
+                else:
+                    proto.hub_eof(err)
+        finally:
+            if view is not None:
+                try:
+                    view.release()
+                except BufferError:  # a consumer kept a slice: never reuse under it
+                    buf = -1
+            if buf >= 0 and not self.closed:
+                core.release(buf)
 
     def stats(self) -> dict:
         return {} if self.closed else dict(self.core.stats(), streams=len(self.protos))
@@ -181,6 +204,7 @@ class WatchReaderHub:
             proto.close()
         self.protos.clear()
         self._flush.clear()
+        self._pending = None
         self.core.close()
 
 

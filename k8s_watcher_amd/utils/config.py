@@ -350,6 +350,11 @@ class WatcherSettings:
     # the kernel (malloc_trim, off the event loop); 0 = never
     malloc_trim_seconds: float = 60.0
     malloc_trim_min_free_mb: float = 16.0  # ... only when the C heap holds at least this much free (retained) memory
+    # once every scope has synced, collect and freeze what start-up left
+    # (gc.freeze): later full collections then walk only objects made since,
+    # not the service's long-lived ones (a 1,000-scope relist storm's gen-2
+    # pauses); unfrozen again at shutdown
+    gc_freeze: bool = True
     shard: "ShardSettings" = field(default_factory=lambda: ShardSettings())
     leader_election: LeaderElectionSettings = field(default_factory=LeaderElectionSettings)
 
@@ -514,6 +519,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
                                            0.0, 86400.0),
         malloc_trim_min_free_mb=_bounded_float(w.get("malloc_trim_min_free_mb", 16.0), "watcher.malloc_trim_min_free_mb",
                                                0.0, 1e6),
+        gc_freeze=_as_bool(w.get("gc_freeze", True), "watcher.gc_freeze"),
         thread_pinning=_choice(w.get("thread_pinning", "auto"), "watcher.thread_pinning", ("auto", "loop", "none")),
         retry=_retry(w.get("retry"), "watcher.retry", RetryPolicy(3, 5.0), min_attempts=0),
         watch_timeout_seconds=_as_int(w.get("watch_timeout_seconds", 300), "watcher.watch_timeout_seconds"),

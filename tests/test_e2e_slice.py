@@ -137,3 +137,27 @@ def test_lifecycle_order_per_pod():
         by_uid.setdefault(p["uid"], []).append(p["event_type"])
     for seq in by_uid.values():
         assert seq == ["ADDED", "MODIFIED", "MODIFIED", "MODIFIED", "DELETED"]
+
+
+@pytest.mark.parametrize("freeze", [True, False])
+def test_gc_freeze_after_sync_and_unfreeze_at_shutdown(freeze):
+    """watcher.gc_freeze: start-up's survivors are frozen once every scope has
+    synced (full collections skip them), and unfrozen at shutdown so a retired
+    service (a leader's last term) is collectable."""
+    import gc
+
+    async def body():
+        srv, sink, svc = await start_stack(overrides={"watcher": {"gc_freeze": freeze}})
+        base = gc.get_freeze_count()
+        await svc.start()
+        during = gc.get_freeze_count()
+        svc.stop()
+        await svc.shutdown()
+        after = gc.get_freeze_count()
+        await sink.stop()
+        await srv.stop()
+        return base, during, after
+
+    base, during, after = run(body())
+    assert base == 0 and after == 0
+    assert (during > 0) == freeze

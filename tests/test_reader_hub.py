@@ -851,3 +851,56 @@ def test_take_dispatch_merges_queued_reads_of_one_stream():
     assert by_uid(got) == by_uid(want)  # per pod, in stream order
     assert cache == {u: list(e) for u, e in want_cache.items()} and rv == want_rv
     assert stats["merged_reads"] > 0 and stats["dispatch_batches"] < stats["reads"], stats
+
+
+def test_dispatch_delivery_is_sliced_across_loop_turns_in_order():
+    """A storm's dispatch (hundreds of reads needing Python at once) is delivered
+    over several loop turns, at most DISPATCH_SLICE_S each, in arrival order; no
+    new take_dispatch runs while a rest is pending (a bound stream's later reads
+    must stay behind its attention read)."""
+
+    class Core:
+        def __init__(self, batches):
+            self.batches, self.takes, self.released = list(batches), 0, []
+
+        def take_dispatch(self):
+            self.takes += 1
+            return self.batches.pop(0) if self.batches else ([], [])
+
+        def release(self, buf):
+            self.released.append(buf)
+
+    class Proto:
+        def __init__(self, log, sid):
+            self.log, self.sid, self.hub_sync = log, sid, None
+
+        def hub_native(self, result, read_ns, done):
+            time.sleep(0.0005)
+            self.log.append((self.sid, result))
+
+        def hub_data(self, view, read_ns):
+            self.log.append((self.sid, bytes(view)))
+
+    async def main():
+        hub = object.__new__(WatchReaderHub)
+        hub.loop = asyncio.get_running_loop()
+        hub.DISPATCH_SLICE_S = 0.002
+        log, turns = [], []
+        first = [(sid, -2, ("r", sid), 1, 0) for sid in range(200)]
+        first.append((7, 3, memoryview(b"later"), 1, 0))  # a plain read of stream 7 behind its attention read
+        second = [(7, -2, ("r2", 7), 1, 0)]
+        hub.core = Core([(first, list(range(200))), (second, [7])])
+        hub.protos = {sid: Proto(log, sid) for sid in range(200)}
+        hub._flush, hub._pending, hub.closed = {"k": lambda: turns.append(len(log))}, None, False
+        hub._on_ready()
+        assert hub._pending is not None and hub.core.takes == 1 and len(log) < 200
+        while hub._pending is not None:
+            hub._on_ready()  # an eventfd wake-up while a rest is pending: delivers the rest, takes nothing
+            assert hub.core.takes == 1 or hub._pending is None
+        hub._on_ready()  # now the next take
+        assert hub.core.takes == 2
+        assert log == [(sid, ("r", sid)) for sid in range(200)] + [(7, b"later"), (7, ("r2", 7))]
+        assert hub.core.released == [3]
+        assert len(turns) >= 3  # flushed after every turn
+
+    run(main())
