@@ -386,14 +386,16 @@ class Fixtures:
             await asyncio.sleep(0.05)
         keys: dict = {}
         total = 0
+        stalls = []
         for f in files:
             with open(f) as fh:
                 doc = json.load(fh)
             total += doc["count"]
             for k, v in doc["keys"].items():
                 keys[k] = keys.get(k, 0) + v
+            stalls += [(t, ms, os.path.basename(f)) for t, ms in doc.get("stalls", ())]
         return {"workers_reporting": len(files), "received": total, "unique": len(keys),
-                "duplicates": sum(v - 1 for v in keys.values() if v > 1)}
+                "duplicates": sum(v - 1 for v in keys.values() if v > 1), "stalls": sorted(stalls)}
 
     async def close(self) -> None:
         if self.replay is not None and self.replay.returncode is None:
@@ -670,6 +672,7 @@ async def rank_main(args, d: Dist) -> dict:
         hub0 = hub.stats() if hub is not None else None
         cpu0 = cpu_snapshot(fx)
         cg0 = cgroup_cpu()
+        t0_mono = time.monotonic()  # the sink's stall times are CLOCK_MONOTONIC
         t0 = time.perf_counter()
         if prof is not None:
             prof.enable()
@@ -775,7 +778,8 @@ async def rank_main(args, d: Dist) -> dict:
                 # (the reference-equivalent speaks plain http to the API server, as
                 # the reference's bench runs do: no figure against an https one)
                 ref = await run_reference(args, fx, shared, targets, k_lat + 1)
-        return {"elapsed": elapsed, "events": events, "notified": notified, "series": series, "rss_mib": rss,
+        return {"elapsed": elapsed, "t0_mono": t0_mono, "events": events, "notified": notified, "series": series,
+                "rss_mib": rss,
                 "timed_seconds": timed_seconds, "lat_hi_seconds": lat_hi_seconds, "lat_seconds": lat_seconds,
                 "lat_io": lat_io,
                 "trims": {"count": c.get("malloc_trims", 0), "skipped": c.get("malloc_trims_skipped", 0),
@@ -907,6 +911,8 @@ class SecondSeries:
 
     def __init__(self, c, metrics, fx: "Fixtures", hub) -> None:
         import gc
+        import numpy
+        self._np = numpy
         self.c, self.metrics, self.fx, self.hub = c, metrics, fx, hub
         self.rows: list = []
         self._gc_ms = 0.0
@@ -966,10 +972,13 @@ class SecondSeries:
             row["sink_cpu"] = round(b["sink_cpu"] - a["sink_cpu"], 3)
         samples = self.metrics.latency.samples
         if samples is not None and b["lat_n"] > a["lat_n"]:
-            new = samples[a["lat_n"]:b["lat_n"]]
-            row["lat_n"] = len(new)
-            row["lat_max_ms"] = round(max(new) / 1e6, 3)
-            row["lat_over_1ms"] = sum(1 for x in new if x > 1_000_000)
+            # numpy over the array's buffer: a Python pass over a second's
+            # ~500k samples held this (measured) loop ~15 ms every second
+            new = self._np.frombuffer(samples, dtype=self._np.int64)[a["lat_n"]:b["lat_n"]]
+            row["lat_n"] = int(new.size)
+            row["lat_max_ms"] = round(int(new.max()) / 1e6, 3)
+            row["lat_over_1ms"] = int((new > 1_000_000).sum())
+            del new  # the array may grow (realloc) only once no view holds its buffer
         self.rows.append(row)
         self._base = b
         self.gap_max = 0.0
@@ -1298,6 +1307,10 @@ def main(argv=None) -> int:
         verify["delivered_by_shards"] = int(delivered_total)
         verify["exactly_once"] = verify["missing"] == 0 and verify["duplicates"] == 0 \
             and verify["received"] == verify["expected"]
+        # the sink's serving-loop turns over 20 ms, at seconds from the start of
+        # the timed steps (negative: warm-up; past timed_seconds: latency phases)
+        verify["stalls"] = [{"at_s": round(t - res["t0_mono"], 3), "ms": round(ms, 1), "worker": w}
+                            for t, ms, w in verify.get("stalls", ())]
     out = {
         "metric": METRIC,
         "value": round(value, 1),

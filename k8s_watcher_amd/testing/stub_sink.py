@@ -295,7 +295,7 @@ def run_sink_process(port: int, workers: int = 1, latency: float = 0.0,
             count, keys = srv.snapshot(reset)
             final = os.path.join(verify_dir, f"sink-{os.getpid()}.json")
             with open(final + ".tmp", "w") as fh:  # renamed when complete: readers never see a partial dump
-                json.dump({"count": count, "keys": keys}, fh)
+                json.dump({"count": count, "keys": keys, "stalls": srv.stalls()}, fh)
             os.replace(final + ".tmp", final)
 
         loop.add_signal_handler(_signal.SIGTERM, stop.set)
