@@ -145,6 +145,8 @@ def parse_args(argv=None):
                     help="https API server (as every real cluster): the replay fixture serves TLS, the watcher "
                          "verifies it against a throw-away CA")
     ap.add_argument("--sink-workers", type=int, default=None, help="default 4 per rank")
+    ap.add_argument("--sink-no-thp", action="store_true",
+                    help="stub clusterapi processes without transparent huge pages (fixture stall A/B)")
     ap.add_argument("--sink-engine", default="auto", choices=["auto", "native", "python"],
                     help="stub clusterapi request loop (auto: native _kwcore.SinkServer unless --tls)")
     ap.add_argument("--fixture-workers", type=int, default=None, help="default 2 per rank")
@@ -349,7 +351,8 @@ class Fixtures:
             sink_ports.append(free_port())
             self.sinks.append(await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.stub_sink",
                                           "--port", str(sink_ports[-1]), "--workers", str(per_sink),
-                                          "--engine", args.sink_engine, *tls_args, *verify, cpus=rank_cpus[g]))
+                                          "--engine", args.sink_engine, *tls_args, *verify,
+                                          *(["--no-thp"] if args.sink_no_thp else []), cpus=rank_cpus[g]))
         line = (await asyncio.wait_for(self.replay.stdout.readline(), 600)).decode()
         assert line.startswith("READY "), line
         self.info = json.loads(line[6:])
@@ -393,7 +396,7 @@ class Fixtures:
             total += doc["count"]
             for k, v in doc["keys"].items():
                 keys[k] = keys.get(k, 0) + v
-            stalls += [(t, ms, os.path.basename(f)) for t, ms in doc.get("stalls", ())]
+            stalls += [(st[0], st[1:], os.path.basename(f)) for st in doc.get("stalls", ())]
         return {"workers_reporting": len(files), "received": total, "unique": len(keys),
                 "duplicates": sum(v - 1 for v in keys.values() if v > 1), "stalls": sorted(stalls)}
 
@@ -1309,8 +1312,10 @@ def main(argv=None) -> int:
             and verify["received"] == verify["expected"]
         # the sink's serving-loop turns over 20 ms, at seconds from the start of
         # the timed steps (negative: warm-up; past timed_seconds: latency phases)
-        verify["stalls"] = [{"at_s": round(t - res["t0_mono"], 3), "ms": round(ms, 1), "worker": w}
-                            for t, ms, w in verify.get("stalls", ())]
+        # and what the sink thread did meanwhile (CPU time, page faults, context switches)
+        verify["stalls"] = [{"at_s": round(t - res["t0_mono"], 3), "ms": round(x[0], 1), "cpu_ms": round(x[1], 1),
+                             "minflt": x[2], "majflt": x[3], "nvcsw": x[4], "nivcsw": x[5], "worker": w}
+                            for t, x, w in verify.get("stalls", ())]
     out = {
         "metric": METRIC,
         "value": round(value, 1),

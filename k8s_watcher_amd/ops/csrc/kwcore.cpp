@@ -31,6 +31,7 @@
 #include <netinet/tcp.h>
 #include <poll.h>
 #include <sys/epoll.h>
+#include <sys/resource.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <sys/syscall.h>

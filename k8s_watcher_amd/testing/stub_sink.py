@@ -359,7 +359,12 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--tls-key", default=None)
     ap.add_argument("--engine", default="auto", choices=["auto", "native", "python"],
                     help="request loop: native (_kwcore.SinkServer) or the asyncio protocol")
+    ap.add_argument("--no-thp", action="store_true",
+                    help="no transparent huge pages for this process and its workers (PR_SET_THP_DISABLE)")
     args = ap.parse_args(argv)
+    if args.no_thp:
+        import ctypes
+        ctypes.CDLL(None, use_errno=True).prctl(41, 1, 0, 0, 0)  # PR_SET_THP_DISABLE, inherited by the forks
     tls = (args.tls_cert, args.tls_key) if args.tls_cert else None
     print(f"stub clusterapi listening on {'https' if tls else 'http'}://127.0.0.1:{args.port}", flush=True)
     run_sink_process(args.port, args.workers, args.latency, args.verify_dir, tls, args.engine, args.expect_keys)

@@ -18,7 +18,8 @@ OUT=${1:?out dir}
 shift
 mkdir -p "$OUT"
 export PYTHONUNBUFFERED=1
-{ date; nproc; python -c "import os; print('affinity', len(os.sched_getaffinity(0)))"; git rev-parse HEAD 2>/dev/null; } > "$OUT/host.txt" 2>&1
+{ date; nproc; python -c "import os; print('affinity', len(os.sched_getaffinity(0)))"; git rev-parse HEAD 2>/dev/null;
+  echo "thp $(cat /sys/kernel/mm/transparent_hugepage/enabled) defrag $(cat /sys/kernel/mm/transparent_hugepage/defrag)"; } > "$OUT/host.txt" 2>&1
 
 fail() { echo "FAILED: $1"; tail -40 "$2"; exit 1; }
 

@@ -153,3 +153,20 @@ def test_native_sink_rejects_bad_fd():
         load().SinkServer(-1)
     with pytest.raises(ValueError):
         load().SinkServer(0, b"/api/pods/update", True, -1)
+
+
+def test_native_sink_reports_stalls_as_a_list():
+    """stalls(): serving-loop turns over 20 ms with the thread's rusage deltas
+    (none on an idle sink); the bench lines them up with its per-second rows."""
+    import socket
+    from k8s_watcher_amd.ops.native import load
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    sock.listen(8)
+    srv = load().SinkServer(sock.fileno(), b"/api/pods/update", True, 16)
+    sock.close()
+    try:
+        st = srv.stalls()
+        assert isinstance(st, list) and all(len(x) == 7 for x in st)
+    finally:
+        srv.close()
