@@ -223,6 +223,12 @@ class WatcherService:
     async def start(self) -> None:
         """Setup + start background tasks; returns once every scope has synced."""
         s = self.settings
+        if s.watcher.gc_freeze:
+            # what import and configuration made is permanent: the full
+            # collections that starting a thousand scopes triggers then walk
+            # only the scopes' own objects (70-140 ms gen-2 pauses otherwise)
+            gc.freeze()
+            self._gc_frozen = True
         if not await self.setup_k8s_client():
             self.log.error("Failed to setup Kubernetes client")
             raise SetupError("Failed to setup Kubernetes client")
@@ -364,7 +370,6 @@ class WatcherService:
         if s.watcher.gc_freeze and not self._stop.is_set():
             gc.collect()
             gc.freeze()
-            self._gc_frozen = True
         self.metrics.ready = True
         self.started.set()
 
