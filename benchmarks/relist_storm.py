@@ -57,6 +57,8 @@ def parse_args(argv=None):
                          "both the initial sync and the post-410 resync")
     ap.add_argument("--sink-workers", type=int, default=2)
     ap.add_argument("--timeout", type=float, default=300.0)
+    ap.add_argument("--slow-ms", type=float, default=10.0,
+                    help="name the loop turns (and collector pauses) longer than this in loop_lag.slow_turns (0: off)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -95,12 +97,20 @@ async def sink_keys(sinks, verify_dir: str, workers: int, sig=signal.SIGUSR1) ->
 
 
 class LagMonitor:
-    """Event-loop scheduling lag: a 1 ms timer, how late it fires."""
+    """Event-loop scheduling lag: a 1 ms timer, how late it fires. With
+    ``slow_ms`` it also names the loop turns that took longer (the callback or
+    task step that ran, where it stood) and the collector pauses, so a lag
+    outlier has a cause in the JSON."""
 
-    def __init__(self) -> None:
+    def __init__(self, slow_ms: float = 0.0) -> None:
         self.max_s = 0.0
         self.samples = []
         self._task = None
+        self.slow_s = slow_ms / 1e3
+        self.slow: list = []
+        self._orig = None
+        self._t0 = 0.0
+        self._gc_t = 0.0
 
     async def _run(self) -> None:
         while True:
@@ -111,15 +121,63 @@ class LagMonitor:
             if lag > self.max_s:
                 self.max_s = lag
 
+    @staticmethod
+    def _name(handle) -> str:
+        cb = handle._callback
+        task = getattr(cb, "__self__", None)
+        if isinstance(task, asyncio.Task):
+            coro = task.get_coro()
+            fr = getattr(coro, "cr_frame", None)
+            where = f"{os.path.basename(fr.f_code.co_filename)}:{fr.f_lineno}" if fr else "done"
+            return f"task {getattr(coro, '__qualname__', coro)} @ {where}"
+        return getattr(cb, "__qualname__", repr(cb))[:80]
+
+    def _gc_cb(self, phase: str, info: dict) -> None:
+        if phase == "start":
+            self._gc_t = time.perf_counter()
+        else:
+            dt = time.perf_counter() - self._gc_t
+            if dt > self.slow_s:
+                self.slow.append((dt, self._gc_t - self._t0, f"gc gen {info['generation']} "
+                                                             f"(collected {info['collected']})"))
+
     def start(self) -> None:
-        self.max_s, self.samples = 0.0, []
+        self.max_s, self.samples, self.slow = 0.0, [], []
+        self._t0 = time.perf_counter()
+        if self.slow_s > 0:
+            import asyncio.events as ev
+            import gc
+            orig = self._orig = ev.Handle._run
+            mon = self
+
+            def _run(handle):
+                t = time.perf_counter()
+                try:
+                    return orig(handle)
+                finally:
+                    dt = time.perf_counter() - t
+                    if dt > mon.slow_s:
+                        mon.slow.append((dt, t - mon._t0, mon._name(handle)))
+
+            ev.Handle._run = _run
+            gc.callbacks.append(self._gc_cb)
         self._task = asyncio.ensure_future(self._run())
 
     def stop(self) -> dict:
         self._task.cancel()
+        if self._orig is not None:
+            import asyncio.events as ev
+            import gc
+            ev.Handle._run = self._orig
+            self._orig = None
+            gc.callbacks.remove(self._gc_cb)
         s = sorted(self.samples) or [0.0]
-        return {"max_ms": round(self.max_s * 1e3, 2), "p99_ms": round(s[int(0.99 * (len(s) - 1))] * 1e3, 2),
-                "p50_ms": round(s[len(s) // 2] * 1e3, 3), "samples": len(s)}
+        out = {"max_ms": round(self.max_s * 1e3, 2), "p99_ms": round(s[int(0.99 * (len(s) - 1))] * 1e3, 2),
+               "p50_ms": round(s[len(s) // 2] * 1e3, 3), "samples": len(s)}
+        if self.slow_s > 0:  # the longest turns, with when (s from the phase's start) and what ran
+            out["slow_turns"] = [{"ms": round(dt * 1e3, 1), "at_s": round(at, 3), "what": what}
+                                 for dt, at, what in sorted(self.slow, reverse=True)[:12]]
+        return out
 
 
 async def wait_quiet(svc, c, relists_target: int, timeout: float) -> None:
@@ -171,7 +229,7 @@ async def main_async(args) -> dict:
         c = metrics.c
         svc = WatcherService(settings, endpoint=KubeEndpoint(server=f"http://127.0.0.1:{info['port']}"),
                              metrics=metrics, serve_metrics=False)
-        lag = LagMonitor()
+        lag = LagMonitor(args.slow_ms)
 
         # ---- initial sync: every pod ADDED once
         lag.start()

@@ -368,7 +368,11 @@ class WatcherService:
             self._on_namespaces(self.ns_watcher.names)  # changes seen while the first scopes started
         await self._wait_synced()
         if s.watcher.gc_freeze and not self._stop.is_set():
-            gc.collect()
+            # the scopes' long-lived objects join the frozen set; only the young
+            # generations are collected first (a full pass over a 1,000-scope
+            # start's objects would hold the loop ~30 ms; cyclic garbage already
+            # in the old generation stays frozen until shutdown unfreezes it)
+            gc.collect(1)
             gc.freeze()
         self.metrics.ready = True
         self.started.set()
