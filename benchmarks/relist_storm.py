@@ -57,15 +57,37 @@ def parse_args(argv=None):
                          "both the initial sync and the post-410 resync")
     ap.add_argument("--sink-workers", type=int, default=2)
     ap.add_argument("--timeout", type=float, default=300.0)
+    ap.add_argument("--fixture-placement", default="apart", choices=["apart", "any"],
+                    help="apart: the fixtures run on other L3 domains than the watcher (off its loop core)")
     ap.add_argument("--slow-ms", type=float, default=10.0,
                     help="name the loop turns (and collector pauses) longer than this in loop_lag.slow_turns (0: off)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
 
-async def spawn(*cmd):
+def fixture_cpus(placement: str):
+    """CPUs for the storm and sink fixtures: ``apart`` = the other L3 domains
+    of this host (the watcher keeps the one it runs on, and its event-loop
+    core is not shared with a fixture's busy process); ``any`` = unpinned."""
+    if placement != "apart":
+        return None
+    from k8s_watcher_amd.utils.cpus import l3_domain_cpus, l3_domains
+    doms = l3_domains()
+    here = l3_domain_cpus()
+    if len(doms) < 2 or not here:
+        return None
+    allowed = os.sched_getaffinity(0)
+    rest = set().union(*(d for d in doms if d != frozenset(here))) & allowed
+    return rest or None
+
+
+async def spawn(*cmd, cpus=None):
+    def pin():
+        if cpus:
+            os.sched_setaffinity(0, cpus)
     return await asyncio.create_subprocess_exec(*cmd, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
-                                                stderr=asyncio.subprocess.DEVNULL, start_new_session=True, cwd=ROOT)
+                                                stderr=asyncio.subprocess.DEVNULL, start_new_session=True, cwd=ROOT,
+                                                preexec_fn=pin if cpus else None)
 
 
 async def command(proc, line: str) -> dict:
@@ -139,7 +161,7 @@ class LagMonitor:
             dt = time.perf_counter() - self._gc_t
             if dt > self.slow_s:
                 self.slow.append((dt, self._gc_t - self._t0, f"gc gen {info['generation']} "
-                                                             f"(collected {info['collected']})"))
+                                                             f"(collected {info['collected']})", None))
 
     def start(self) -> None:
         self.max_s, self.samples, self.slow = 0.0, [], []
@@ -150,14 +172,17 @@ class LagMonitor:
             orig = self._orig = ev.Handle._run
             mon = self
 
+            thread_time = time.thread_time
+
             def _run(handle):
+                c = thread_time()
                 t = time.perf_counter()
                 try:
                     return orig(handle)
                 finally:
                     dt = time.perf_counter() - t
-                    if dt > mon.slow_s:
-                        mon.slow.append((dt, t - mon._t0, mon._name(handle)))
+                    if dt > mon.slow_s:  # with the loop thread's CPU time over it: work, or waiting
+                        mon.slow.append((dt, t - mon._t0, mon._name(handle), thread_time() - c))
 
             ev.Handle._run = _run
             gc.callbacks.append(self._gc_cb)
@@ -175,8 +200,9 @@ class LagMonitor:
         out = {"max_ms": round(self.max_s * 1e3, 2), "p99_ms": round(s[int(0.99 * (len(s) - 1))] * 1e3, 2),
                "p50_ms": round(s[len(s) // 2] * 1e3, 3), "samples": len(s)}
         if self.slow_s > 0:  # the longest turns, with when (s from the phase's start) and what ran
-            out["slow_turns"] = [{"ms": round(dt * 1e3, 1), "at_s": round(at, 3), "what": what}
-                                 for dt, at, what in sorted(self.slow, reverse=True)[:12]]
+            out["slow_turns"] = [{"ms": round(dt * 1e3, 1), "cpu_ms": None if cpu is None else round(cpu * 1e3, 1),
+                                  "at_s": round(at, 3), "what": what}
+                                 for dt, at, what, cpu in sorted(self.slow, key=lambda x: -x[0])[:12]]
         return out
 
 
@@ -201,8 +227,9 @@ async def main_async(args) -> dict:
     server = sinks = None
     try:
         t_fix = time.perf_counter()
+        fx_cpus = fixture_cpus(args.fixture_placement)
         server = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.storm_server", "--namespaces",
-                             str(args.namespaces), "--pods", str(args.pods), "--out-dir", out_dir)
+                             str(args.namespaces), "--pods", str(args.pods), "--out-dir", out_dir, cpus=fx_cpus)
         line = (await asyncio.wait_for(server.stdout.readline(), 600)).decode()
         assert line.startswith("READY "), line
         info = json.loads(line[6:])
@@ -211,7 +238,7 @@ async def main_async(args) -> dict:
             s.bind(("127.0.0.1", 0))
             sink_port = s.getsockname()[1]
         sinks = [await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.stub_sink", "--port", str(sink_port),
-                             "--workers", str(args.sink_workers), "--engine", "native", "--verify-dir", verify_dir)]
+                             "--workers", str(args.sink_workers), "--engine", "native", "--verify-dir", verify_dir, cpus=fx_cpus)]
         await asyncio.wait_for(sinks[0].stdout.readline(), 60)
         await asyncio.sleep(0.3)
         fixture_s = time.perf_counter() - t_fix
@@ -291,7 +318,8 @@ async def main_async(args) -> dict:
             "config": {"namespaces": args.namespaces, "pods": info["pods"], "scope": args.scope, "scopes": scopes,
                        "churn": args.churn, "relist_slice_ms": args.slice_ms, "relist_concurrency": args.concurrency,
                        "list_page_size": args.page, "profile": "staging", "engine": "native",
-                       "initial_sync": args.initial_sync},
+                       "initial_sync": args.initial_sync,
+                       "fixture_cpus": len(fx_cpus) if fx_cpus else "any"},
             "fixture_setup_s": round(fixture_s, 2),
             "initial": {"wall_s": round(initial_s, 3), "watcher_cpu_s": cpu(cpu0, cpu1), "loop_lag": initial_lag,
                         "relist": slices(initial_slices), "exactly_once": initial_ok, "notified": len(keys0)},
