@@ -226,14 +226,23 @@ def memory_census(top: int = 40) -> Dict[str, object]:
     # garbage the collector has not reached yet (a closed connection's
     # transport <-> protocol cycle waits for a gen-2 pass: 23 "extra"
     # transports in a soak's census diff were exactly that)
+    # (watcher.gc_freeze) frozen objects are invisible to get_objects() and
+    # never collected: thaw them for the count, report how many there were and
+    # how much of them had become garbage (the freeze's one-time cost), and
+    # freeze what is still live again
+    frozen = gc.get_freeze_count()
+    if frozen:
+        gc.unfreeze()
     collected = gc.collect()
     counts: Dict[str, int] = {}
     for o in gc.get_objects():
         t = type(o)
         k = f"{t.__module__}.{t.__qualname__}"
         counts[k] = counts.get(k, 0) + 1
+    if frozen:
+        gc.freeze()
     out: Dict[str, object] = {
-        "gc_objects": sum(counts.values()), "garbage_collected": collected,
+        "gc_objects": sum(counts.values()), "garbage_collected": collected, "frozen_before": frozen,
         "allocated_blocks": sys.getallocatedblocks(),
         "types": dict(sorted(counts.items(), key=lambda kv: -kv[1])[:top]), "gc_counts": list(gc.get_count())}
     if tracemalloc.is_tracing():

@@ -176,3 +176,24 @@ def test_debug_memory_endpoint_only_when_enabled():
     assert doc["gc_objects"] > 1000 and "builtins.dict" in doc["types"]
     assert doc["garbage_collected"] >= 0  # counted after a collection: live objects only
     assert doc["tracemalloc"]["traced_bytes"] > 0 and doc["tracemalloc"]["top"]
+
+
+def test_memory_census_counts_frozen_objects_and_keeps_them_frozen():
+    """With watcher.gc_freeze the census thaws the frozen set to count it (and
+    to collect any of it that became garbage), then freezes what is live again."""
+    import gc
+    from k8s_watcher_amd.metrics import memory_census
+
+    class Marker:
+        pass
+
+    keep = [Marker() for _ in range(50)]
+    gc.freeze()
+    try:
+        doc = memory_census(top=1000)
+        assert doc["frozen_before"] > 0
+        assert doc["types"].get(f"{Marker.__module__}.{Marker.__qualname__}", 0) >= 50
+        assert gc.get_freeze_count() > 0
+    finally:
+        gc.unfreeze()
+    del keep
