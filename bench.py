@@ -1223,6 +1223,11 @@ def soak_report(args, d: "Dist", res: dict) -> int:
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    # what the service does at start() in a deployment, where its process is
+    # still single-threaded then; here the process group and asyncio's child
+    # watcher start threads before the service does (utils/fds.py)
+    from k8s_watcher_amd.utils.fds import reserve_fd_table
+    reserve_fd_table(16384)
     d = Dist()
     res = asyncio.run(rank_main(args, d))
     if res.get("soak"):

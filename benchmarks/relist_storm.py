@@ -163,8 +163,28 @@ class LagMonitor:
                 self.slow.append((dt, self._gc_t - self._t0, f"gc gen {info['generation']} "
                                                              f"(collected {info['collected']})", None))
 
+    def _watch(self, loop_tid: int) -> None:
+        # a thread that samples the loop thread's Python stack while a turn
+        # runs long: it gets the GIL only if the loop released it (blocked in
+        # C code or descheduled outside a GIL section), so a stack here says
+        # which call the loop sat in; none says it held the GIL throughout
+        import sys
+        import traceback
+        while not self._stop_watch:
+            time.sleep(0.005)
+            t = self._turn_t
+            if t and time.perf_counter() - t > self.slow_s:
+                fr = sys._current_frames().get(loop_tid)
+                if fr is not None:
+                    st = traceback.extract_stack(fr)[-6:]
+                    key = " <- ".join(f"{os.path.basename(f.filename)}:{f.lineno}:{f.name}" for f in reversed(st))
+                    self.stacks[key] = self.stacks.get(key, 0) + 1
+
     def start(self) -> None:
         self.max_s, self.samples, self.slow = 0.0, [], []
+        self.stacks = {}
+        self._turn_t = 0.0
+        self._stop_watch = False
         self._t0 = time.perf_counter()
         if self.slow_s > 0:
             import asyncio.events as ev
@@ -176,16 +196,20 @@ class LagMonitor:
 
             def _run(handle):
                 c = thread_time()
-                t = time.perf_counter()
+                t = mon._turn_t = time.perf_counter()
                 try:
                     return orig(handle)
                 finally:
+                    mon._turn_t = 0.0
                     dt = time.perf_counter() - t
                     if dt > mon.slow_s:  # with the loop thread's CPU time over it: work, or waiting
                         mon.slow.append((dt, t - mon._t0, mon._name(handle), thread_time() - c))
 
             ev.Handle._run = _run
             gc.callbacks.append(self._gc_cb)
+            import threading
+            self._watcher = threading.Thread(target=self._watch, args=(threading.get_ident(),), daemon=True)
+            self._watcher.start()
         self._task = asyncio.ensure_future(self._run())
 
     def stop(self) -> dict:
@@ -196,6 +220,8 @@ class LagMonitor:
             ev.Handle._run = self._orig
             self._orig = None
             gc.callbacks.remove(self._gc_cb)
+            self._stop_watch = True
+            self._watcher.join()
         s = sorted(self.samples) or [0.0]
         out = {"max_ms": round(self.max_s * 1e3, 2), "p99_ms": round(s[int(0.99 * (len(s) - 1))] * 1e3, 2),
                "p50_ms": round(s[len(s) // 2] * 1e3, 3), "samples": len(s)}
@@ -203,6 +229,9 @@ class LagMonitor:
             out["slow_turns"] = [{"ms": round(dt * 1e3, 1), "cpu_ms": None if cpu is None else round(cpu * 1e3, 1),
                                   "at_s": round(at, 3), "what": what}
                                  for dt, at, what, cpu in sorted(self.slow, key=lambda x: -x[0])[:12]]
+            # where the loop thread stood while a turn ran long (5 ms samples)
+            out["slow_turn_stacks"] = [{"samples": n, "stack": k}
+                                       for k, n in sorted(self.stacks.items(), key=lambda kv: -kv[1])[:8]]
         return out
 
 
@@ -348,6 +377,11 @@ async def main_async(args) -> dict:
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    # what the service does at start() in a deployment, where its process is
+    # still single-threaded then; here asyncio's child watcher has started a
+    # thread per fixture by the time the service starts (utils/fds.py)
+    from k8s_watcher_amd.utils.fds import reserve_fd_table
+    reserve_fd_table(16384)
     res = asyncio.run(main_async(args))
     line = json.dumps(res)
     print(line, flush=True)

@@ -223,6 +223,12 @@ class WatcherService:
     async def start(self) -> None:
         """Setup + start background tasks; returns once every scope has synced."""
         s = self.settings
+        if s.watcher.fd_table_reserve:
+            # before the decode pool, reader and I/O threads exist: growing a
+            # shared descriptor table later stalls the opening thread ~150 ms
+            # per doubling on a 256-CPU host (utils/fds.py)
+            from ..utils.fds import reserve_fd_table
+            reserve_fd_table(s.watcher.fd_table_reserve)
         if s.watcher.gc_freeze:
             # what import and configuration made is permanent: the full
             # collections that starting a thousand scopes triggers then walk

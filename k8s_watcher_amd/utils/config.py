@@ -355,6 +355,10 @@ class WatcherSettings:
     # not the service's long-lived ones (a 1,000-scope relist storm's gen-2
     # pauses); unfrozen again at shutdown
     gc_freeze: bool = True
+    # the descriptor table grown once at start to hold this many fds (a watch
+    # per namespace opens two each; growing it later, with threads running,
+    # waits an RCU grace period per doubling: utils/fds.py); 0 = as needed
+    fd_table_reserve: int = 16384
     shard: "ShardSettings" = field(default_factory=lambda: ShardSettings())
     leader_election: LeaderElectionSettings = field(default_factory=LeaderElectionSettings)
 
@@ -520,6 +524,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         malloc_trim_min_free_mb=_bounded_float(w.get("malloc_trim_min_free_mb", 16.0), "watcher.malloc_trim_min_free_mb",
                                                0.0, 1e6),
         gc_freeze=_as_bool(w.get("gc_freeze", True), "watcher.gc_freeze"),
+        fd_table_reserve=max(0, _as_int(w.get("fd_table_reserve", 16384), "watcher.fd_table_reserve")),
         thread_pinning=_choice(w.get("thread_pinning", "auto"), "watcher.thread_pinning", ("auto", "loop", "none")),
         retry=_retry(w.get("retry"), "watcher.retry", RetryPolicy(3, 5.0), min_attempts=0),
         watch_timeout_seconds=_as_int(w.get("watch_timeout_seconds", 300), "watcher.watch_timeout_seconds"),
