@@ -145,8 +145,17 @@ async def run_ours(srv: Servers, profile: str, overrides: dict, steps: List[str]
     list_p50 = m.latency.percentile_ns(50)
     startup = {"delivered": c["notify_delivered"], "seconds": time.perf_counter() - t_start,
                "p50_ms": (list_p50 / 1e6) if list_p50 else None}
+    def settle() -> None:
+        # the notifier's I/O thread hands latency samples over in blocks: take
+        # what it holds at a phase's end, so they do not land in the next phase
+        # (they had put the saturated phase's tail into config #3's paced p50)
+        flush = getattr(svc.notifier, "flush", None)
+        if flush is not None:
+            flush()
+
     for s in warm_steps:
         await until_idle(c["events_received"], await srv.cmd(s))
+    settle()
     m.latency.reset()
     n0, d0 = c["events_received"], c["notify_delivered"]
     t0 = time.perf_counter()
@@ -168,6 +177,7 @@ async def run_ours(srv: Servers, profile: str, overrides: dict, steps: List[str]
             await asyncio.sleep(0.0005)
     elapsed = time.perf_counter() - t0
     events = c["events_received"] - n0
+    settle()
     sat_p50 = m.latency.percentile_ns(50)
     out = {"events": events, "seconds": elapsed, "events_per_s": events / elapsed if elapsed else None,
            "notified": c["notify_delivered"] - d0,
@@ -175,6 +185,7 @@ async def run_ours(srv: Servers, profile: str, overrides: dict, steps: List[str]
     if pace:
         m.latency.reset()
         await until_idle(c["events_received"], await srv.cmd(pace))
+        settle()
         p50, p99 = m.latency.percentile_ns(50), m.latency.percentile_ns(99)
         out.update({"p50_ms": p50 / 1e6 if p50 else None, "p99_ms": p99 / 1e6 if p99 else None,
                     "latency_samples": m.latency.n})
