@@ -341,11 +341,15 @@ class Fixtures:
         if args.verify:
             self.verify_dir = tempfile.mkdtemp(prefix="bench-verify-")
             verify = ["--verify-dir", self.verify_dir]
-            # distinct keys per sink worker over the run (x2: connections need not spread
-            # evenly): the native sink sizes its table for them instead of rehashing mid-run
+            # distinct keys per sink worker over the run: the native sink sizes its
+            # table for them instead of rehashing mid-run. Every worker is sized
+            # for its front-end's whole share: SO_REUSEPORT hashes the notifier's
+            # few connections onto the workers, and one worker holding most of
+            # them rehashed ~4M keys mid-run (a 316 ms stall, 16k page faults,
+            # profiles/r4/final/bench_h1.json)
             total = ((args.warmup + args.steps) * args.pods_per_step * world * args.rounds_per_step * 5
                      * (0.2 if args.profile == "production" else 1.0))
-            verify += ["--expect-keys", str(min(8 << 20, int(total * 2 / max(1, per_sink * fronts))))]
+            verify += ["--expect-keys", str(min(16 << 20, int(total * 1.05 / max(1, fronts))))]
         sink_ports = []
         for g in range(fronts):
             sink_ports.append(free_port())

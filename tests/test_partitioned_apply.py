@@ -131,3 +131,103 @@ def test_partitioned_apply_under_many_small_and_large_batches():
     for piece in (9000, 40 * 1024, len(data)):
         got = feed("staging", {}, data, partitioned=True, piece=piece)
         assert per_uid(got[0]) == per_uid(base[0]) and got[1] == base[1] and got[2] == base[2], piece
+
+
+def feed_group(data_by_ns, partitioned):
+    """Several namespace pipelines sharing one pod cache and native notifier
+    (the discover shape), bound to one reader hub: take_dispatch runs their
+    reads as group batches, partitioned or not."""
+    import os
+    import socket
+    import threading
+    import time
+    from test_reader_hub import _chunked, _dispatch_until
+
+    async def body():
+        sink = StubSink()
+        await sink.start()
+        s = load_settings("staging", overrides={"clusterapi": {"base_url": sink.url, "health_check_on_start": False},
+                                                "watcher": {"namespace_scope": "discover"}}, environ={})
+        m = Metrics()
+        pool = NativeNotifierPool(s.clusterapi, m)
+        kw = load()
+        dpool = kw.DecodePool(3)
+        core = kw.ReaderHub(256 * 1024, 32)
+        first = None
+        pipes, socks, sids = {}, [], {}
+        for ns in data_by_ns:
+            p = EventPipeline(s, PyDecoder("staging"), pool, m, cache=first.cache if first else None)
+            first = first or p
+            p.log_events_setting = False
+            p.attach_native(dpool)
+            p.sync_native_log()
+            a, b = socket.socketpair()
+            sid = core.add(os.dup(b.fileno()))
+            core.bind(sid, p.native, True)
+            pipes[ns], sids[sid] = p, ns
+            socks += [a, b]
+        prev = kw.set_partitioned_apply(partitioned)
+        kw.probe(True)
+        senders = [threading.Thread(target=socks[2 * i].sendall, args=(_chunked(d, piece=5000),), daemon=True)
+                   for i, d in enumerate(data_by_ns.values())]
+        for t in senders:
+            t.start()
+        time.sleep(0.2)
+        done = []
+
+        def on_item(it):
+            sid, buf, view, read_ns, err = it
+            p = pipes[sids[sid]]
+            if buf == -2:
+                p.native_result(view, read_ns)
+                if err:
+                    done.append(sid)
+                return
+            if view is not None:
+                p.native_result(p.native.feed_chunked(view, read_ns), read_ns)
+                if p.native.body_done():
+                    done.append(sid)
+                view.release()
+                core.release(buf)
+
+        try:
+            _dispatch_until(core, lambda: len(done) == len(pipes), on_item, timeout=60)
+        finally:
+            probe = kw.probe(False)
+            kw.set_partitioned_apply(prev)
+        for t in senders:
+            t.join()
+        assert await pool.drain(20)
+        got = [(x["uid"], x["event_type"], x["status"]["phase"]) for x in sink.state.payloads()]
+        rvs = {ns: p.native.last_rv() for ns, p in pipes.items()}
+        cache = {u: [e[0], e[1], e[2], e[3]] for u, e in first.cache.items()}
+        for sid in sids:
+            core.unbind(sid)
+        core.close()
+        for x in socks:
+            x.close()
+        await pool.close()
+        await sink.stop()
+        dpool.close()
+        return got, rvs, cache, probe
+
+    return run(body(), timeout=120)
+
+
+def test_partitioned_group_batches_keep_each_namespace_resume_point():
+    """Group batches of many namespace watches (one pipeline each, one shared
+    cache): the partitioned apply leaves every pipeline the resume point, the
+    notifications and the cache the serial apply does — the resume walk stops
+    once every pipeline of the batch has its own resourceVersion."""
+    lines = [event_line(t, o) for t, o in churn_events(400, seed=5, namespaces=NAMESPACES)]
+    by_ns = {ns: [] for ns in NAMESPACES}
+    for ln in lines:
+        by_ns[json.loads(ln)["object"]["metadata"]["namespace"]].append(ln)
+    data = {ns: b"".join(v) for ns, v in by_ns.items() if v}
+    s_got, s_rvs, s_cache, _ = feed_group(data, partitioned=False)
+    p_got, p_rvs, p_cache, p_probe = feed_group(data, partitioned=True)
+    assert p_probe["partitioned_batches"] > 0
+    assert p_rvs == s_rvs and all(s_rvs.values())
+    assert collections.Counter(p_got) == collections.Counter(s_got)
+    assert per_uid(p_got) == per_uid(s_got)
+    assert p_cache == s_cache
