@@ -55,6 +55,7 @@ class WatchReaderHub:
         self._tls: Dict[tuple, object] = {}
         self._flush: Dict[object, object] = {}  # bind(): once per dispatch
         self._pending = None  # (items, touched) a dispatch's delivery left for the next turn
+        self._soon = None  # the loop turn scheduled to deliver it
         self._fd = self.core.fileno()
         self.loop.add_reader(self._fd, self._on_ready)
         self.closed = False
@@ -123,9 +124,15 @@ class WatchReaderHub:
         if not self.closed:
             self.core.pause(sid, paused)
 
+    def _continue(self) -> None:
+        self._soon = None
+        self._on_ready()
+
     def _on_ready(self) -> None:
         core = self.core
         if self._pending is not None:  # the rest of the last dispatch first: no newer read may pass it
+            if self._soon is not None:
+                return  # the eventfd, still readable: the turn scheduled for the rest delivers it
             items, touched = self._pending
             self._pending = None
         else:
@@ -168,7 +175,7 @@ class WatchReaderHub:
                 self._deliver_read(core, sid, buf, view, read_ns, err)
             if i < last and not self.closed and time.perf_counter() > deadline:
                 self._pending = (items[i + 1:], touched)
-                self.loop.call_soon(self._on_ready)
+                self._soon = self.loop.call_soon(self._continue)
                 return
 
     def _deliver_read(self, core, sid, buf, view, read_ns, err) -> None:
@@ -205,6 +212,9 @@ class WatchReaderHub:
         self.protos.clear()
         self._flush.clear()
         self._pending = None
+        if self._soon is not None:
+            self._soon.cancel()
+            self._soon = None
         self.core.close()
 
 

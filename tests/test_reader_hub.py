@@ -891,11 +891,14 @@ def test_dispatch_delivery_is_sliced_across_loop_turns_in_order():
         second = [(7, -2, ("r2", 7), 1, 0)]
         hub.core = Core([(first, list(range(200))), (second, [7])])
         hub.protos = {sid: Proto(log, sid) for sid in range(200)}
-        hub._flush, hub._pending, hub.closed = {"k": lambda: turns.append(len(log))}, None, False
+        hub._flush, hub._pending, hub._soon, hub.closed = {"k": lambda: turns.append(len(log))}, None, None, False
         hub._on_ready()
         assert hub._pending is not None and hub.core.takes == 1 and len(log) < 200
+        n = len(log)
+        hub._on_ready()  # an eventfd wake-up while a rest is pending: the scheduled turn delivers it
+        assert len(log) == n and hub.core.takes == 1
         while hub._pending is not None:
-            hub._on_ready()  # an eventfd wake-up while a rest is pending: delivers the rest, takes nothing
+            await asyncio.sleep(0)  # the scheduled turns deliver the rest, taking nothing new
             assert hub.core.takes == 1 or hub._pending is None
         hub._on_ready()  # now the next take
         assert hub.core.takes == 2
