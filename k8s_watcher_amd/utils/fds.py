@@ -12,8 +12,8 @@ held the event loop that long five times, once per doubling from 128 to 4,096
 ``socket()`` with ~0.2 ms of CPU over each stall).
 
 :func:`reserve_fd_table` grows the table once, up front, to the size the
-service will need: a ``dup2`` onto a high descriptor number, closed again at
-once. The table keeps its size (it never shrinks), so later sockets fit
+service will need: a duplicate at a high descriptor number (``F_DUPFD``),
+closed again at once. The table keeps its size (it never shrinks), so later sockets fit
 without a growth. Done while the process still has one thread, the growth does
 not wait for a grace period at all. The soft ``RLIMIT_NOFILE`` is raised to the
 reservation (within the hard limit) first, as a watch per namespace needs it.
@@ -21,6 +21,7 @@ reservation (within the hard limit) first, as a watch per namespace needs it.
 
 from __future__ import annotations
 
+import fcntl
 import os
 import resource
 from typing import Optional
@@ -57,13 +58,13 @@ def reserve_fd_table(n: int) -> int:
         return size or 0
     fd = os.open(os.devnull, os.O_RDONLY | os.O_CLOEXEC)
     try:
+        # F_DUPFD: the lowest free descriptor >= top (never one another thread
+        # holds, as dup2 onto a fixed number could be); the table grows to fit it
         try:
-            os.fstat(top)
-            return fd_table_size() or 0  # already open: the table holds it
-        except OSError:
-            pass
-        os.dup2(fd, top, inheritable=False)
-        os.close(top)
+            high = fcntl.fcntl(fd, fcntl.F_DUPFD_CLOEXEC, top)
+        except OSError:  # EMFILE / EINVAL: at the limit already
+            return fd_table_size() or 0
+        os.close(high)
     finally:
         os.close(fd)
     return fd_table_size() or 0
