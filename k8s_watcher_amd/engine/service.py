@@ -311,7 +311,8 @@ class WatcherService:
                                                   max_bytes=s.watcher.watch_reader_max_bytes,
                                                   frame=s.watcher.hub_framing,
                                                   recv_slice=s.watcher.watch_recv_slice,
-                                                  depth=s.watcher.watch_reader_depth)
+                                                  depth=s.watcher.watch_reader_depth,
+                                                  frame_defer=s.watcher.hub_frame_defer)
                 self.api.http.reader_hub = self._reader_hub
                 hub = self._reader_hub
                 self.metrics.gauges["watch_reader_streams"] = lambda: float(len(hub.protos))

@@ -567,7 +567,7 @@ def test_busy_streams_grow_only_to_their_share_of_the_pool():
         b.close()
 
 
-@pytest.mark.parametrize("recv_slice", [0, 4096, 5000])
+@pytest.mark.parametrize("recv_slice", [0, 4096, 5000, "defer"])
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_hub_framing_matches_pipeline_framing_on_random_chunking(seed, recv_slice):
     """Once a chunked body is bound, the hub frames it (chunk de-framing and
@@ -576,7 +576,10 @@ def test_hub_framing_matches_pipeline_framing_on_random_chunking(seed, recv_slic
     chunk headers, line ends and buffer ends everywhere — the result is
     identical to the pipeline framing the same bytes itself. With a recv
     slice (watcher.watch_recv_slice) each recv() of a buffer is framed on its
-    own, so slice ends land everywhere too."""
+    own, so slice ends land everywhere too. "defer": whole-buffer reads with
+    watcher.hub_frame_defer — a read that fills its small buffer leaves the
+    stream's framing to take() until it has caught up, so the framing moves
+    between the reader thread and the consumer mid-stream, repeatedly."""
     import random
     import threading
     from test_native_pipeline import Recorder, run_native, stream
@@ -602,8 +605,11 @@ def test_hub_framing_matches_pipeline_framing_on_random_chunking(seed, recv_slic
     p.attach_native(load().DecodePool(2))
     p.sync_native_log()
     core = load().ReaderHub(16 * 1024, 16)
+    defer = recv_slice == "defer"
+    recv_slice = 0 if defer else recv_slice
     core.set_recv_slice(recv_slice)
-    assert core.stats()["recv_slice"] == recv_slice
+    core.set_frame_defer(defer)
+    assert core.stats()["recv_slice"] == recv_slice and core.stats()["frame_defer"] == defer
     a, b = socket.socketpair()
     sid = core.add(os.dup(b.fileno()))
     core.bind(sid, p.native, True)
@@ -639,6 +645,8 @@ def test_hub_framing_matches_pipeline_framing_on_random_chunking(seed, recv_slic
     st = core.stats()
     assert st["framed_reads"] > 0 and st["frame_ns"] > 0  # the hub did frame (after the first take)
     assert st["recv_bytes"] == len(raw) and st["recv_ns"] > 0
+    if defer:  # the reader fell behind and handed framing over, and the consumer framed
+        assert st["deferred_reads"] > 0 and st["consumer_frame_ns"] > 0
     core.close()
     a.close()
     b.close()
