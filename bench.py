@@ -112,7 +112,7 @@ def parse_args(argv=None):
     ap.add_argument("--watch-reader-max-bytes", type=int, default=None, help="watcher.watch_reader_max_bytes")
     ap.add_argument("--reader-depth", type=int, default=None, help="watcher.watch_reader_depth (buffers per stream)")
     ap.add_argument("--recv-slice", type=int, default=None, help="watcher.watch_recv_slice (bytes per recv, framed in L2)")
-    ap.add_argument("--frame-defer", default=None, choices=["on", "off"],
+    ap.add_argument("--frame-defer", default=None, choices=["off", "caught_up", "per_read"],
                     help="watcher.hub_frame_defer: a reader behind its socket leaves framing to the loop")
     ap.add_argument("--thread-pinning", default=None, choices=["auto", "loop", "none"], help="watcher.thread_pinning")
     ap.add_argument("--no-placement", dest="placement", action="store_false",
@@ -500,7 +500,7 @@ async def rank_main(args, d: Dist) -> dict:
                            if args.watch_reader_max_bytes is not None else {}),
                         **({"watch_recv_slice": args.recv_slice} if args.recv_slice is not None else {}),
                         **({"watch_reader_depth": args.reader_depth} if args.reader_depth is not None else {}),
-                        **({"hub_frame_defer": args.frame_defer == "on"} if args.frame_defer else {}),
+                        **({"hub_frame_defer": args.frame_defer} if args.frame_defer else {}),
                         **({"thread_pinning": args.thread_pinning} if args.thread_pinning else {}),
                         **({"validate": args.validate} if args.validate else {}),
                         **({"hub_dispatch": args.hub_dispatch == "on"} if args.hub_dispatch else {}),

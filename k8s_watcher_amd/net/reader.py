@@ -38,7 +38,7 @@ class WatchReaderHub:
 
     def __init__(self, buf_bytes: int, nbufs: int = 64,
                  loop: Optional[asyncio.AbstractEventLoop] = None, max_bytes: int = 0, frame: bool = True,
-                 recv_slice: int = 0, depth: int = 2, frame_defer: bool = False) -> None:
+                 recv_slice: int = 0, depth: int = 2, frame_defer: str = "off") -> None:
         self.loop = loop or asyncio.get_running_loop()
         # max_bytes: read-ahead over all streams (0: the whole pool); frame: the
         # hub's thread de-chunks and splits bound bodies (watcher.hub_framing)
@@ -53,8 +53,9 @@ class WatchReaderHub:
             self.core.set_depth(int(depth))
         # frame_defer: a reader behind its socket leaves framing to the loop's
         # take until it has caught up (watcher.hub_frame_defer)
-        if frame_defer:
-            self.core.set_frame_defer(True)
+        mode = {"off": 0, "caught_up": 1, "per_read": 2}[frame_defer]
+        if mode:
+            self.core.set_frame_defer(mode)
         self.protos: Dict[int, object] = {}
         self._tls: Dict[tuple, object] = {}
         self._flush: Dict[object, object] = {}  # bind(): once per dispatch

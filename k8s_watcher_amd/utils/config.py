@@ -325,7 +325,9 @@ class WatcherSettings:
     watch_reader_depth: int = 2  # ReaderHub read-ahead per stream, in buffers (2..8)
     # a reader thread behind its socket (a read filled its buffer) leaves the
     # framing of that stream to the event loop's take until it has caught up
-    hub_frame_defer: bool = False
+    # (off | caught_up: until the loop has caught up | per_read: each read
+    # that fills its buffer on its own)
+    hub_frame_defer: str = "off"
     hub_dispatch: bool = True  # hub-read watches feed the native pipeline with no Python call per read
     hub_framing: bool = True  # ... and the hub's thread de-chunks and splits their bodies (readerhub.inc HubFramer)
     partitioned_apply: bool = True  # a batch's apply split by pod-cache shard over the decode pool (engine.inc)
@@ -519,7 +521,8 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         watch_reader_max_bytes=max(0, _as_int(w.get("watch_reader_max_bytes", 0), "watcher.watch_reader_max_bytes")),
         watch_recv_slice=_recv_slice(w.get("watch_recv_slice", 0)),
         watch_reader_depth=_reader_depth(w.get("watch_reader_depth", 2)),
-        hub_frame_defer=_as_bool(w.get("hub_frame_defer", False), "watcher.hub_frame_defer"),
+        hub_frame_defer=_choice(w.get("hub_frame_defer", "off"), "watcher.hub_frame_defer",
+                                ("off", "caught_up", "per_read")),
         hub_dispatch=_as_bool(w.get("hub_dispatch", True), "watcher.hub_dispatch"),
         hub_framing=_as_bool(w.get("hub_framing", True), "watcher.hub_framing"),
         partitioned_apply=_as_bool(w.get("partitioned_apply", True), "watcher.partitioned_apply"),

@@ -567,7 +567,7 @@ def test_busy_streams_grow_only_to_their_share_of_the_pool():
         b.close()
 
 
-@pytest.mark.parametrize("recv_slice", [0, 4096, 5000, "defer"])
+@pytest.mark.parametrize("recv_slice", [0, 4096, 5000, "defer", "defer_per_read"])
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_hub_framing_matches_pipeline_framing_on_random_chunking(seed, recv_slice):
     """Once a chunked body is bound, the hub frames it (chunk de-framing and
@@ -605,7 +605,7 @@ def test_hub_framing_matches_pipeline_framing_on_random_chunking(seed, recv_slic
     p.attach_native(load().DecodePool(2))
     p.sync_native_log()
     core = load().ReaderHub(16 * 1024, 16)
-    defer = recv_slice == "defer"
+    defer = {"defer": 1, "defer_per_read": 2}.get(recv_slice, 0)
     recv_slice = 0 if defer else recv_slice
     core.set_recv_slice(recv_slice)
     core.set_frame_defer(defer)
