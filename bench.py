@@ -434,6 +434,13 @@ class Fixtures:
             shutil.rmtree(self.verify_dir, ignore_errors=True)
 
 
+def progress(d: "Dist", what: str) -> None:
+    """A line on stderr per phase (rank 0): a multi-rank run under a
+    supervisor that takes minutes of silence for a hang keeps showing life."""
+    if d.rank == 0:
+        print(f"bench: {what}", file=sys.stderr, flush=True)
+
+
 async def rank_main(args, d: Dist) -> dict:
     from k8s_watcher_amd.engine.service import WatcherService
     from k8s_watcher_amd.kube.kubeconfig import KubeEndpoint
@@ -658,6 +665,7 @@ async def rank_main(args, d: Dist) -> dict:
                            "all_events": ((t_all or t_end) - t_start) / steps, "drained": (t_end - t_start) / steps})
             await d.abarrier()
 
+        progress(d, f"service up ({scope}), warm-up: {args.warmup} steps")
         for k in range(args.warmup):
             await run_step(k, per_step)
         getattr(svc.notifier, "flush", lambda: None)()  # the warm-up's samples the I/O thread still holds
@@ -688,6 +696,7 @@ async def rank_main(args, d: Dist) -> dict:
             prof.enable()
         phases.clear()
         timed_seconds: list = []
+        progress(d, f"timed: {args.steps} steps")
         if args.step_sync == "stream":
             await run_stream(args.warmup, args.steps, per_step, timed_seconds)
         else:
@@ -743,6 +752,7 @@ async def rank_main(args, d: Dist) -> dict:
         settle_samples()
         sat = list(metrics.latency.samples or [])
 
+        progress(d, f"timed steps done in {elapsed:.1f} s; latency phases")
         # latency at the nominal rate, per rank (untimed)
         metrics.latency.reset()
         k_lat = (args.warmup + args.steps) * R
@@ -791,6 +801,7 @@ async def rank_main(args, d: Dist) -> dict:
             if args.ref_events > 0 and not args.api_tls:
                 # (the reference-equivalent speaks plain http to the API server, as
                 # the reference's bench runs do: no figure against an https one)
+                progress(d, "reference-equivalent pipeline")
                 ref = await run_reference(args, fx, shared, targets, k_lat + 1)
         return {"elapsed": elapsed, "t0_mono": t0_mono, "events": events, "notified": notified, "series": series,
                 "rss_mib": rss,
@@ -1266,6 +1277,7 @@ def main(argv=None) -> int:
         a2.ref_events = 0
         a2.warmup = min(args.warmup, 2)
         a2.steps = max(4, args.steps // 2)
+        progress(d, "second placement (fixtures apart)")
         r2 = asyncio.run(rank_main(a2, d))
         el2 = d.reduce(r2["elapsed"], "MAX")
         ev2 = d.reduce(float(r2["events"]), "SUM")
@@ -1292,6 +1304,7 @@ def main(argv=None) -> int:
         a3.warmup = 1
         a3.steps = max(1, args.staging_steps)
         a3.fixture_placement = args.fixture_placement
+        progress(d, "staging phase (every event notified)")
         r3 = asyncio.run(rank_main(a3, d))
         el3 = d.reduce(r3["elapsed"], "MAX")
         ev3 = d.reduce(float(r3["events"]), "SUM")
