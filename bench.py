@@ -967,6 +967,8 @@ class SecondSeries:
         if self.hub is not None:
             st = self.hub.stats()
             out["starved"] = st.get("starved", 0)
+            out["recv_ns"], out["recv_bytes"] = st.get("recv_ns", 0), st.get("recv_bytes", 0)
+            out["frame_ns"] = st.get("frame_ns", 0)
         if self.fx.replay is not None:
             cpu = cpu_snapshot(self.fx, threads=False)
             out["replay_cpu"], out["sink_cpu"] = cpu["replay"], cpu["sink"]
@@ -992,6 +994,13 @@ class SecondSeries:
                "trims": b["trims"] - a["trims"], "trim_ms": round((b["trim_us"] - a["trim_us"]) / 1e3, 2)}
         if "starved" in b:
             row["reader_starved"] = b["starved"] - a["starved"]
+            # the reader thread in that second: share of it in recv / framing, and
+            # the recv copy's rate (the headline's bound: a second where every
+            # stage slows at once shows here if the copy did)
+            dr = b["recv_ns"] - a["recv_ns"]
+            row["reader_recv"] = round(dr / 1e9, 3)
+            row["reader_frame"] = round((b["frame_ns"] - a["frame_ns"]) / 1e9, 3)
+            row["reader_gb_s"] = round((b["recv_bytes"] - a["recv_bytes"]) / dr, 2) if dr else 0.0
         if "replay_cpu" in b:
             row["replay_cpu"] = round(b["replay_cpu"] - a["replay_cpu"], 3)
             row["sink_cpu"] = round(b["sink_cpu"] - a["sink_cpu"], 3)
