@@ -275,7 +275,9 @@ class Soak:
         for k in ("cached_pods", "cache_bytes", "notify_outstanding", "notify_outstanding_bytes",
                   "watch_reader_allocated_bytes", "watch_reader_held_bytes", "malloc_in_use_bytes", "malloc_free_bytes",
                   "checkpoint_stall_ms", "checkpoint_write_ms", "checkpoint_bytes", "events_received",
-                  "notify_delivered", "expired_410", "watch_restarts", "relists", "bookmarks"):
+                  "notify_delivered", "expired_410", "watch_restarts", "relists", "bookmarks",
+                  "apply_partitioned_batches", "apply_partitioned_lines", "apply_tail_serial_lines",
+                  "apply_tail_submits", "apply_tail_lock_runs", "apply_serial_batches", "apply_serial_lines"):
             if k in m:
                 s[k] = m[k]
         self.samples.append(s)

@@ -298,7 +298,12 @@ class WatcherService:
                                       event_sharding=self._event_sharding())
         if self._native_pipeline():
             from ..ops.native import load as _load_native
-            _load_native().set_partitioned_apply(s.watcher.partitioned_apply)
+            _kw = _load_native()
+            _kw.set_partitioned_apply(s.watcher.partitioned_apply)
+            # which apply path ran, and how much of it (cumulative, process-wide)
+            for _key in ("partitioned_batches", "partitioned_lines", "tail_serial_lines", "tail_submits",
+                         "tail_lock_runs", "serial_batches", "serial_lines"):
+                self.metrics.gauges["apply_" + _key] = (lambda k=_key: float(_kw.apply_stats()[k]))
             self._decode_pool = self._make_decode_pool()
             self.pipeline.attach_native(self._decode_pool)
             http = self.api.http

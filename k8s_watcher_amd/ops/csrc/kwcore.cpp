@@ -2143,6 +2143,8 @@ PyMethodDef module_methods[] = {
      "stamp_fields(buf, rv_off, rvs, ndigits, uid_off, uid_text): fixture re-stamping (int64 arrays)"},
     {"cpu_features", (PyCFunction)kw_cpu_features, METH_NOARGS, "SIMD paths in use"},
     {"set_simd", (PyCFunction)kw_set_simd, METH_O, "enable/disable the AVX2 scanner"},
+    {"apply_stats", (PyCFunction)kw_apply_stats, METH_NOARGS,
+     "apply_stats() -> cumulative counts of the partitioned and serial apply paths"},
     {"probe", (PyCFunction)kw_probe, METH_O, "probe(enable) -> event-loop thread time in native calls since the last call"},
     {"set_partitioned_apply", (PyCFunction)kw_set_partitioned_apply, METH_O,
      "set_partitioned_apply(on) -> previous: batches' apply phase split by pod-cache shard over the decode pool"},
