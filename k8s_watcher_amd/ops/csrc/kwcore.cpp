@@ -2073,6 +2073,7 @@ PyObject* kw_bench_parse(PyObject*, PyObject* args) {
 #include "relist.inc"
 #include "readerhub.inc"
 #include "sinkserver.inc"
+#include "looplag.inc"
 
 // json_invalid(data) -> None if json.loads(data) accepts it, else the reason (validate.inc)
 PyObject* kw_json_invalid(PyObject*, PyObject* arg) {
@@ -2179,7 +2180,8 @@ PyMODINIT_FUNC PyInit__kwcore(void) {
     Py_INCREF(&ScannerType);
     PyModule_AddObject(m, "ResponseScanner", (PyObject*)&ScannerType);
     if (register_engine(m) < 0 || register_podcache(m) < 0 || register_pipeline(m) < 0 || register_logsink(m) < 0 ||
-        register_checkpoint(m) < 0 || register_relist(m) < 0 || register_readerhub(m) < 0 || register_sinkserver(m) < 0)
+        register_checkpoint(m) < 0 || register_relist(m) < 0 || register_readerhub(m) < 0 || register_sinkserver(m) < 0 ||
+        register_looplag(m) < 0)
         return nullptr;
     const char* names[6] = {"ADDED", "MODIFIED", "DELETED", "BOOKMARK", "ERROR", "INVALID"};
     for (int i = 0; i < 6; ++i) {

@@ -345,6 +345,14 @@ def run_sink_process(port: int, workers: int = 1, latency: float = 0.0,
         asyncio.run(serve_native() if engine == "native" else serve())
     except KeyboardInterrupt:
         pass
+    # the workers got the same SIGTERM (one process group) and may still be
+    # writing their final dump: the parent outlives them, so whoever waits for
+    # it waits for the whole sink (nothing is left behind for init to reap)
+    for pid in pids:
+        try:
+            os.waitpid(pid, 0)
+        except ChildProcessError:
+            pass
 
 
 def main(argv: Optional[List[str]] = None) -> None:

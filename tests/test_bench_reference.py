@@ -8,23 +8,21 @@ per step cut the reference to two thirds of its 1-round rate and inflated
 ``vs_baseline`` ~3x. Now the fixture answers from an index and the clock
 starts at the first paced event."""
 
-import json
 import os
-import subprocess
-import sys
+
+from conftest import run_bench  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _bench(rounds: int) -> dict:
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
-                        "--pods-per-step", "2000", "--rounds-per-step", str(rounds), "--namespaces", "8",
-                        "--ref-events", "1500", "--latency-seconds", "0.5", "--latency-seconds-high", "0",
-                        "--staging", "off", "--apart", "off", "--no-verify", "--sink-workers", "1",
-                        "--no-placement"],
-                       capture_output=True, text=True, timeout=600, cwd=ROOT)
-    assert r.returncode == 0, r.stderr[-3000:]
-    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])["reference_equiv"]
+    d = run_bench(["--steps", "2", "--warmup", "1",
+                   "--pods-per-step", "2000", "--rounds-per-step", str(rounds), "--namespaces", "8",
+                   "--ref-events", "1500", "--latency-seconds", "0.5", "--latency-seconds-high", "0",
+                   "--staging", "off", "--apart", "off", "--no-verify", "--sink-workers", "1",
+                   "--no-placement"])
+    assert d["_headline"]["reference_equiv_events_per_s"] == d["reference_equiv"]["events_per_s"]
+    return d["reference_equiv"]
 
 
 def test_reference_rate_independent_of_history_length():

@@ -12,7 +12,7 @@ import sys
 
 import pytest
 
-from conftest import ROOT
+from conftest import ROOT, run_bench
 
 pytestmark = pytest.mark.gpu
 
@@ -31,11 +31,8 @@ def test_smoke_end_to_end():
 
 
 def test_bench_line_is_valid():
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off",
-                          "--pods-per-step", "1000", "--ref-events", "500", "--latency-seconds", "1", "--latency-seconds-high", "1"],
-                         capture_output=True, text=True, timeout=600, cwd=ROOT)
-    assert out.returncode == 0, out.stderr[-2000:]
-    line = json.loads(out.stdout.strip().splitlines()[-1])
+    line = run_bench(["--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off",
+                          "--pods-per-step", "1000", "--ref-events", "500", "--latency-seconds", "1", "--latency-seconds-high", "1"])
     for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "vs_baseline"):
         assert key in line
     assert line["value"] > 0 and line["n_gpus"] == 1 and line["steps"] == 2
@@ -47,12 +44,9 @@ def test_bench_line_is_valid():
 
 def test_https_api_server_bench_line_is_valid():
     """An https API server (every real cluster) through the hub's native TLS on the host."""
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off",
+    line = run_bench(["--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off",
                           "--pods-per-step", "1000", "--ref-events", "0", "--latency-seconds", "1",
-                          "--latency-rate-high", "0", "--api-tls"],
-                         capture_output=True, text=True, timeout=600, cwd=ROOT)
-    assert out.returncode == 0, out.stderr[-2000:]
-    line = json.loads(out.stdout.strip().splitlines()[-1])
+                          "--latency-rate-high", "0", "--api-tls"])
     assert line["config"]["api_server"] == "https" and line["verify"]["exactly_once"]
     assert line["watch_reader_rank0"]["mode"] == "native"
 
@@ -84,13 +78,10 @@ def test_hub_framing_and_grouped_dispatch_on_host():
             test_reader_hub.test_hub_framing_matches_pipeline_framing_on_random_chunking(seed, recv_slice)
     test_reader_hub.test_take_dispatch_groups_many_bound_streams_like_serial_feeding()
     test_reader_hub.test_busy_streams_grow_only_to_their_share_of_the_pool()
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+    line = run_bench(["--steps", "2", "--warmup", "1",
                           "--rounds-per-step", "1", "--apart", "off", "--staging", "off", "--ref-events", "0",
                           "--latency-seconds", "0", "--latency-seconds-high", "0", "--watch-scope", "discover",
-                          "--namespaces", "1000"],
-                         capture_output=True, text=True, timeout=600, cwd=ROOT)
-    assert out.returncode == 0, out.stderr[-2000:]
-    line = json.loads(out.stdout.strip().splitlines()[-1])
+                          "--namespaces", "1000"])
     assert line["verify"]["exactly_once"] and line["per_rank"][0]["scopes"] == 1000
     hub = line["watch_reader_rank0"]
     assert hub["mode"] == "native" and hub["framed_reads"] > 0 and hub["hub_dispatch_watches"] == 1000
@@ -109,11 +100,8 @@ def test_native_sink_on_host(tmp_path):
 
 def test_tls_bench_line_is_valid():
     """production.yaml's https clusterapi through the native TLS notifier core, on the host."""
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off",
-                          "--pods-per-step", "1000", "--ref-events", "0", "--latency-seconds", "1", "--latency-rate-high", "0", "--tls"],
-                         capture_output=True, text=True, timeout=600, cwd=ROOT)
-    assert out.returncode == 0, out.stderr[-2000:]
-    line = json.loads(out.stdout.strip().splitlines()[-1])
+    line = run_bench(["--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off",
+                          "--pods-per-step", "1000", "--ref-events", "0", "--latency-seconds", "1", "--latency-rate-high", "0", "--tls"])
     assert line["config"]["clusterapi"] == "https" and line["value"] > 0 and line["notify_failed"] == 0
 
 
@@ -138,12 +126,9 @@ def test_round4_paths_on_host():
     for env, ov in test_partitioned_apply.PROFILES:
         test_partitioned_apply.test_partitioned_apply_matches_serial(env, ov)
     test_reader_hub.test_take_dispatch_merges_queued_reads_of_one_stream()
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+    line = run_bench(["--steps", "3", "--warmup", "1",
                           "--rounds-per-step", "4", "--apart", "off", "--staging", "off", "--ref-events", "0",
-                          "--latency-seconds", "0", "--latency-seconds-high", "2", "--probe"],
-                         capture_output=True, text=True, timeout=600, cwd=ROOT)
-    assert out.returncode == 0, out.stderr[-2000:]
-    line = json.loads(out.stdout.strip().splitlines()[-1])
+                          "--latency-seconds", "0", "--latency-seconds-high", "2", "--probe"])
     assert line["verify"]["exactly_once"] and line["config"]["partitioned_apply"] == "on"
     assert line["loop_probe_rank0"]["partitioned_batches"] > 0
     assert sum(s.get("*", {}).get("bytes", 0) for s in line["fixture_zero_copy"]) > 0
@@ -154,3 +139,13 @@ def test_round4_paths_on_host():
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
     d = json.loads(res.stdout.strip().splitlines()[-1])
     assert d["initial"]["exactly_once"] and d["storm"]["exactly_once"] and d["server"]["lists"] == 0
+
+
+def test_bench_headline_driver_shape_on_host(tmp_path):
+    """The driver's command shape on the host (every phase on, --pods-per-step
+    shortened): the last stdout line is the < 4,096-byte headline, stderr is one
+    line, every 1k ev/s second with a > 1 ms notification names a cause, and no
+    process of the bench outlives it (VERDICT round 4, next #1 / #8)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import test_bench_headline as tbh
+    tbh.check_headline(*tbh.run_driver_shape(tmp_path, extra=("--pods-per-step", "2000")))

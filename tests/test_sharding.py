@@ -14,7 +14,7 @@ import time
 
 import pytest
 
-from conftest import ROOT, run
+from conftest import ROOT, run, run_bench
 from k8s_watcher_amd.parallel.shard import ShardFilter, shard_of
 from k8s_watcher_amd.testing.fake_apiserver import FakeApiServer, ServerThread
 from k8s_watcher_amd.testing.podgen import PodFactory
@@ -119,18 +119,13 @@ def test_bench_sharded_ranks_exactly_once(ranks, assignment, decode):
     assignment for dynamic namespace sets (parallel/shard.py)."""
     port = free_port()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", BENCH_DEBUG="1")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
-                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-                        "--gpus", str(ranks), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off", "--pods-per-step", "300",
-                        "--namespaces", "16", "--ref-events", "0", "--latency-seconds", "0.5", "--latency-seconds-high", "0.5",
-                        "--sink-workers", "2" if ranks < 8 else "1", "--fixture-workers", "2" if ranks < 8 else "1",
-                        "--no-placement", "--assignment", assignment,
-                        "--decode-threads", decode, "--step-timeout", "90"],
-                       capture_output=True, text=True, timeout=900, cwd=ROOT, env=env)
-    assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1  # rank 0 only
-    d = json.loads(lines[0])
+    d = run_bench(["--gpus", str(ranks), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off",
+                   "--staging", "off", "--pods-per-step", "300",
+                   "--namespaces", "16", "--ref-events", "0", "--latency-seconds", "0.5", "--latency-seconds-high", "0.5",
+                   "--sink-workers", "2" if ranks < 8 else "1", "--fixture-workers", "2" if ranks < 8 else "1",
+                   "--no-placement", "--assignment", assignment,
+                   "--decode-threads", decode, "--step-timeout", "90"],
+                  timeout=900, env=env, torchrun_ranks=ranks, port=port)  # one headline line: rank 0's
     assert d["n_gpus"] == ranks and d["config"]["global_batch"] == ranks * 1500
     assert d["value"] > 0 and d["scaling"] == "weak"
     assert "namespace_scope=discover" in d["config"]["parallelism"]
@@ -143,21 +138,18 @@ def test_bench_sharded_ranks_exactly_once(ranks, assignment, decode):
     if decode == "auto":  # 8 local ranks share this container's CPUs: no rank plans more than its share
         from k8s_watcher_amd.utils.cpus import available_cpus
         assert d["config"]["decode_threads"] <= max(0, available_cpus() // ranks - 2)
-    assert sum(p["events"] for p in d["per_rank"]) == 2 * ranks * 1500, (d["per_rank"], r.stderr[-3000:])
+    assert sum(p["events"] for p in d["per_rank"]) == 2 * ranks * 1500, d["per_rank"]
     v = d["verify"]
-    assert v["exactly_once"] and v["duplicates"] == 0 and v["missing"] == 0, (v, r.stderr[-3000:])
+    assert v["exactly_once"] and v["duplicates"] == 0 and v["missing"] == 0, v
     assert v["expected"] == v["delivered_by_shards"] > 0
 
 
 @pytest.mark.parametrize("step_sync", ["stream", "barrier"])
 def test_bench_single_rank_cluster_watch(step_sync):
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off",
+    d = run_bench(["--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off",
                         "--pods-per-step", "300", "--namespaces", "8", "--ref-events", "200",
                         "--latency-seconds", "0.5", "--latency-seconds-high", "0.5", "--sink-workers", "1", "--no-placement",
-                        "--step-sync", step_sync],
-                       capture_output=True, text=True, timeout=600, cwd=ROOT)
-    assert r.returncode == 0, r.stderr[-3000:]
-    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+                        "--step-sync", step_sync])
     assert d["step_sync"] == step_sync
     assert d["n_gpus"] == 1 and d["config"]["parallelism"] == "single-process (cluster watch)"
     assert d["per_rank"][0]["events"] == 2 * 1500
@@ -169,12 +161,9 @@ def test_bench_single_rank_cluster_watch(step_sync):
 def test_bench_https_api_server_through_the_native_reader():
     """bench.py --api-tls: the replay API server speaks TLS (as every real
     cluster does) and the watcher's hub runs the session natively."""
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off",
+    d = run_bench(["--steps", "2", "--warmup", "1", "--rounds-per-step", "1", "--apart", "off", "--staging", "off",
                         "--pods-per-step", "300", "--namespaces", "8", "--ref-events", "0", "--api-tls",
-                        "--latency-seconds", "0.5", "--latency-seconds-high", "0.5", "--sink-workers", "1", "--no-placement"],
-                       capture_output=True, text=True, timeout=600, cwd=ROOT)
-    assert r.returncode == 0, r.stderr[-3000:]
-    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+                        "--latency-seconds", "0.5", "--latency-seconds-high", "0.5", "--sink-workers", "1", "--no-placement"])
     assert d["config"]["api_server"] == "https" and d["verify"]["exactly_once"]
     assert d["watch_reader_rank0"]["mode"] == "native" and d["watch_reader_rank0"]["reads"] > 0
     assert d["watch_reader_rank0"]["hub_dispatch_watches"] > 0  # TLS watches are fed natively too
@@ -444,14 +433,11 @@ def test_bench_sustained_rounds_and_apart_placement():
     fixtures placed apart is reported beside it, and a staging-profile run
     (every event notified: saturated rate, p99 at a fixed rate) — all
     exactly-once."""
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+    d = run_bench(["--steps", "3", "--warmup", "1",
                         "--rounds-per-step", "3", "--apart", "on", "--pods-per-step", "300", "--namespaces", "8",
                         "--staging-steps", "2", "--staging-latency-rate", "2000",
                         "--ref-events", "0", "--latency-seconds", "0.5", "--latency-seconds-high", "0",
-                        "--sink-workers", "1", "--no-placement"],
-                       capture_output=True, text=True, timeout=600, cwd=ROOT)
-    assert r.returncode == 0, r.stderr[-3000:]
-    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+                        "--sink-workers", "1", "--no-placement"])
     assert d["config"]["global_batch"] == 3 * 1500 and d["config"]["rounds_per_step"] == 3
     assert d["per_rank"][0]["events"] == 3 * 3 * 1500
     assert d["verify"]["exactly_once"]
@@ -471,14 +457,11 @@ def test_bench_saturated_soak_mode():
     """bench.py --soak-minutes: chunks streamed back to back, each checked
     exactly-once on its own (the sink is counted and cleared between them),
     RSS after every chunk and its slope."""
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--soak-minutes", "0.08",
+    d = run_bench(["--soak-minutes", "0.08",
                         "--soak-chunk-steps", "2", "--rounds-per-step", "2", "--pods-per-step", "300",
                         "--namespaces", "8", "--warmup", "1", "--apart", "off", "--staging", "off",
                         "--latency-seconds", "0", "--latency-seconds-high", "0", "--ref-events", "0",
-                        "--sink-workers", "1", "--no-placement"],
-                       capture_output=True, text=True, timeout=600, cwd=ROOT)
-    assert r.returncode == 0, r.stderr[-3000:]
-    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+                        "--sink-workers", "1", "--no-placement"])
     assert d["chunks"] >= 2 and d["exactly_once_all"] and d["duplicates"] == 0 and d["missing"] == 0
     assert d["events"] == d["chunks"] * 2 * 2 * 1500 and d["value"] > 0
     assert d["rss_mib"]["max"] >= d["rss_mib"]["first"] > 0
