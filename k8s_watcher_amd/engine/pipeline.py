@@ -277,8 +277,8 @@ class EventPipeline:
             uid = ev[E_UID]
             seen.add(uid)
             ent = cache.get(uid)
-            if ent is None:
-                out.append(ev)
+            if ent is None:  # a WatchList's MODIFIED of an uncached pod is an ADDED too
+                out.append(ev if ev[E_TYPE] == ADDED else (ADDED,) + ev[1:])
             elif ent[0] != ev[E_RV]:
                 out.append((MODIFIED,) + ev[1:])
         for uid, ent in cache.items():

@@ -330,7 +330,8 @@ class Reflector:
                             await asyncio.sleep(0)
                         queued[0] -= len(payload)
                     elif kind == 1:  # DELETED during the initial events: the watch path
-                        for ev in pipe.native_result(native.feed(payload, read_ns), read_ns):
+                        # (cache-only when the sync does not notify, as the Relist's pages)
+                        for ev in pipe.native_result(native.feed(payload, read_ns, not notify), read_ns):
                             self._handle_control(ev)
                         queued[0] -= len(payload)
                     elif kind == 2:

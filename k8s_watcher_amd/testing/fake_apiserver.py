@@ -137,6 +137,9 @@ class FakeApiServer:
                  watch_list: bool = True) -> None:
         self.token = token
         self.watch_list = watch_list  # serve sendInitialEvents=true (WatchList)
+        # test hook: raw events a WatchList's initial stream carries after its
+        # ADDED set (a server interleaving live events before the end bookmark)
+        self.watch_list_inject: List[Dict[str, Any]] = []
         self.history_limit = history_limit
         self.extra_namespaces = list(namespaces or ["default", "kube-system"])
         self.expired_as_http_status = expired_as_http_status
@@ -636,6 +639,8 @@ class FakeApiServer:
             if w.wants(p):
                 writer.write(_chunk(json.dumps({"type": "ADDED", "object": p}, separators=(",", ":"),
                                                ensure_ascii=False).encode() + b"\n"))
+        for ev in self.watch_list_inject:
+            writer.write(_chunk(json.dumps(ev, separators=(",", ":"), ensure_ascii=False).encode() + b"\n"))
         end = {"type": "BOOKMARK", "object": {"kind": "Pod", "apiVersion": "v1", "metadata": {
             "resourceVersion": str(self.rv), "annotations": {"k8s.io/initial-events-end": "true"}}}}
         writer.write(_chunk(json.dumps(end, separators=(",", ":")).encode() + b"\n"))

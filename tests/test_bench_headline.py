@@ -124,8 +124,10 @@ def test_attribution_names_the_segment_that_took_the_time():
 
 
 def test_loop_lag_probe_sees_a_blocked_loop():
-    """_kwcore.LoopLag: a 5 ms block of the loop shows as ~5 ms lag; an idle
-    loop's ticks are answered in well under a millisecond."""
+    """_kwcore.LoopLag: a 20 ms block of the loop shows as a lag of that
+    order (the ticker thread itself may be preempted on a loaded test box, so
+    the bound is loose); an idle loop's ticks are answered in well under a
+    millisecond."""
     import asyncio
     import time
 
@@ -139,7 +141,7 @@ def test_loop_lag_probe_sees_a_blocked_loop():
         p.take()
         await asyncio.sleep(0.3)
         idle = p.take()
-        time.sleep(0.005)  # block the loop
+        time.sleep(0.02)  # block the loop
         await asyncio.sleep(0.05)
         blocked = p.take()
         loop.remove_reader(p.fd())
@@ -148,5 +150,5 @@ def test_loop_lag_probe_sees_a_blocked_loop():
 
     idle, blocked = asyncio.run(body())
     assert idle["n"] >= 300  # ~600 ticks at 500 us; a loaded test box may skip some
-    assert blocked["max_us"] >= 4000 and blocked["over_1ms"] >= 1
+    assert blocked["max_us"] >= 10000 and blocked["over_1ms"] >= 1
     assert idle["over_1ms"] <= 3, idle  # the shared CPU may preempt the loop once in a while

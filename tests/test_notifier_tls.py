@@ -14,7 +14,7 @@ from k8s_watcher_amd.parallel.native_notifier import NativeNotifierPool
 from k8s_watcher_amd.parallel.notifier import NotifierPool
 from k8s_watcher_amd.testing.certs import make_pki
 from k8s_watcher_amd.testing.stub_sink import StubSink
-from test_notifier import TS, core, settings
+from test_notifier import TS, _threaded_native, core, settings
 
 
 @pytest.fixture(scope="module")
@@ -22,9 +22,12 @@ def pki(tmp_path_factory):
     return make_pki(str(tmp_path_factory.mktemp("pki")))
 
 
-@pytest.fixture(params=["python", "native"])
+@pytest.fixture(params=["python", "native", "native-io-thread"])
 def pool_cls(request):
-    return NotifierPool if request.param == "python" else NativeNotifierPool
+    """The native core runs TLS from the event loop and, with
+    ``pool.io_thread``, on its I/O thread (SSL_read / SSL_write outside the
+    core lock)."""
+    return {"python": NotifierPool, "native": NativeNotifierPool, "native-io-thread": _threaded_native}[request.param]
 
 
 async def tls_sink(pki, **kw):

@@ -176,3 +176,63 @@ def test_native_watch_list_large_sync_is_sliced_and_exactly_once():
     # bounded slices: each step of the Relist is budgeted (4 ms here; a 20k-pod
     # reconcile of the Python path ran as one loop slice of ~0.5 s)
     assert d["initial"]["relist"]["max_slice_ms"] < 200 and d["storm"]["relist"]["max_slice_ms"] < 200
+
+
+@pytest.mark.parametrize("engine", ["native", "python"])
+def test_watch_list_skip_initial_deleted_is_silent(engine):
+    """``initial_list: skip`` on a WatchList sync whose initial events carry a
+    DELETED (a server interleaving a live deletion before the end bookmark):
+    the cache forgets the pod, and nothing is sent — on the native path the
+    DELETED goes through the watch path with the pipeline's silent flag, as
+    the Relist's pages do (round-4 advisor finding)."""
+    async def body():
+        f = PodFactory(seed=26, namespaces=["default"])
+        pods = [f.running(f.new_pod()) for _ in range(4)]
+        ov = {"watcher": {**WL["watcher"], "initial_list": "skip"}}
+        srv, sink, svc = await start_stack("development", overrides=ov, engine=engine, pods=pods)
+        gone = pods[1]
+        srv.watch_list_inject = [{"type": "DELETED", "object": gone}]
+        await svc.start()
+        await asyncio.wait_for(svc.reflectors[0].connected.wait(), 5)
+        await asyncio.sleep(0.3)
+        assert svc.metrics.c["watch_list_syncs"] == 1
+        assert sink.state.payloads() == []  # the primed state and the DELETED are both silent
+        p = f.running(f.new_pod("default"))
+        srv.create(p)
+        await sink.state.wait_for(1, timeout=10)
+        await asyncio.sleep(0.2)
+        assert [(g["event_type"], g["uid"]) for g in sink.state.payloads()] == [("ADDED", p["metadata"]["uid"])]
+        svc.stop()
+        await svc.shutdown()
+        await sink.stop()
+        await srv.stop()
+    run(body())
+
+
+@pytest.mark.parametrize("engine", ["native", "python"])
+def test_watch_list_uid_twice_in_initial_events(engine):
+    """A pod whose ADDED and a later MODIFIED both arrive in the initial
+    events (one read): never two ADDEDs. The native collector closes its Relist
+    page at the repeated uid, so the MODIFIED is compared with the ADDED
+    (ADDED, then MODIFIED); the Python path keeps one entry per uid (ADDED of
+    the final state)."""
+    async def body():
+        f = PodFactory(seed=27, namespaces=["default"])
+        pods = [f.running(f.new_pod()) for _ in range(3)]
+        srv, sink, svc = await start_stack("development", overrides=WL, engine=engine, pods=pods)
+        later = dict(pods[0])
+        later["metadata"] = dict(later["metadata"], resourceVersion=str(10 ** 6))
+        later["status"] = dict(later["status"], phase="Succeeded")
+        srv.watch_list_inject = [{"type": "MODIFIED", "object": later}]
+        await svc.start()
+        await sink.state.wait_for(3, timeout=10)
+        await asyncio.sleep(0.3)
+        uid = pods[0]["metadata"]["uid"]
+        types = [g["event_type"] for g in sink.state.payloads() if g["uid"] == uid]
+        assert types == (["ADDED", "MODIFIED"] if engine == "native" else ["ADDED"])
+        assert sorted({g["uid"] for g in sink.state.payloads()}) == sorted(p["metadata"]["uid"] for p in pods)
+        svc.stop()
+        await svc.shutdown()
+        await sink.stop()
+        await srv.stop()
+    run(body())
