@@ -111,9 +111,6 @@ def parse_args(argv=None):
     ap.add_argument("--watch-reader-buffers", type=int, default=None, help="watcher.watch_reader_buffers")
     ap.add_argument("--watch-reader-max-bytes", type=int, default=None, help="watcher.watch_reader_max_bytes")
     ap.add_argument("--reader-depth", type=int, default=None, help="watcher.watch_reader_depth (buffers per stream)")
-    ap.add_argument("--recv-slice", type=int, default=None, help="watcher.watch_recv_slice (bytes per recv, framed in L2)")
-    ap.add_argument("--frame-defer", default=None, choices=["off", "caught_up", "per_read"],
-                    help="watcher.hub_frame_defer: a reader behind its socket leaves framing to the loop")
     ap.add_argument("--thread-pinning", default=None, choices=["auto", "loop", "none"], help="watcher.thread_pinning")
     ap.add_argument("--no-placement", dest="placement", action="store_false",
                     help="no per-rank L3 domain assignment (each watcher still pins per watcher.decode_affinity)")
@@ -152,9 +149,9 @@ def parse_args(argv=None):
     ap.add_argument("--sink-engine", default="auto", choices=["auto", "native", "python"],
                     help="stub clusterapi request loop (auto: native _kwcore.SinkServer unless --tls)")
     ap.add_argument("--fixture-workers", type=int, default=None, help="default 2 per rank")
-    ap.add_argument("--fixture-zero-copy", default="auto", choices=["auto", "warm", "off"],
-                    help="replay fixture sends large watch scopes with sendfile from a memfd ring (auto), each "
-                         "slice read into the cache first (warm), or copies every byte into the socket (off)")
+    ap.add_argument("--fixture-zero-copy", default="auto", choices=["auto", "off"],
+                    help="replay fixture sends large watch scopes with sendfile from a memfd ring (auto), or "
+                         "copies every byte into the socket (off)")
     ap.add_argument("--no-verify", dest="verify", action="store_false",
                     help="sink does not count payload keys (no exactly-once proof)")
     ap.add_argument("--latency-rate", type=float, default=100.0, help="ev/s per rank in the latency phase")
@@ -536,9 +533,7 @@ async def rank_main(args, d: Dist) -> dict:
                         **({"watch_reader_buffers": args.watch_reader_buffers} if args.watch_reader_buffers else {}),
                         **({"watch_reader_max_bytes": args.watch_reader_max_bytes}
                            if args.watch_reader_max_bytes is not None else {}),
-                        **({"watch_recv_slice": args.recv_slice} if args.recv_slice is not None else {}),
                         **({"watch_reader_depth": args.reader_depth} if args.reader_depth is not None else {}),
-                        **({"hub_frame_defer": args.frame_defer} if args.frame_defer else {}),
                         **({"thread_pinning": args.thread_pinning} if args.thread_pinning else {}),
                         **({"validate": args.validate} if args.validate else {}),
                         **({"hub_dispatch": args.hub_dispatch == "on"} if args.hub_dispatch else {}),
@@ -747,10 +742,6 @@ async def rank_main(args, d: Dist) -> dict:
             reader_timed = {"recv_frac": round(dr / 1e9 / elapsed, 3), "frame_frac": round(df / 1e9 / elapsed, 3),
                             "recv_gb_per_s": round(db / dr, 2) if dr else None,
                             "bytes_per_event": round(db / max(1, c["events_received"] - n0))}
-            if hub1.get("frame_defer"):  # framing the loop's take did for a lagging reader
-                reader_timed["loop_frame_frac"] = round((hub1["consumer_frame_ns"] - hub0["consumer_frame_ns"])
-                                                        / 1e9 / elapsed, 3)
-                reader_timed["deferred_reads"] = hub1["deferred_reads"] - hub0["deferred_reads"]
         zc = None
         if d.rank == 0:  # the replay fixture's zero-copy sends (bytes, slot waits) so far
             reply = await fx.cmd("ZCSTATS")

@@ -315,9 +315,7 @@ class WatcherService:
                                                   s.watcher.watch_reader_buffers,
                                                   max_bytes=s.watcher.watch_reader_max_bytes,
                                                   frame=s.watcher.hub_framing,
-                                                  recv_slice=s.watcher.watch_recv_slice,
-                                                  depth=s.watcher.watch_reader_depth,
-                                                  frame_defer=s.watcher.hub_frame_defer)
+                                                  depth=s.watcher.watch_reader_depth)
                 self.api.http.reader_hub = self._reader_hub
                 hub = self._reader_hub
                 self.metrics.gauges["watch_reader_streams"] = lambda: float(len(hub.protos))

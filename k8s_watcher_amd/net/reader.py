@@ -38,24 +38,15 @@ class WatchReaderHub:
 
     def __init__(self, buf_bytes: int, nbufs: int = 64,
                  loop: Optional[asyncio.AbstractEventLoop] = None, max_bytes: int = 0, frame: bool = True,
-                 recv_slice: int = 0, depth: int = 2, frame_defer: str = "off") -> None:
+                 depth: int = 2) -> None:
         self.loop = loop or asyncio.get_running_loop()
         # max_bytes: read-ahead over all streams (0: the whole pool); frame: the
         # hub's thread de-chunks and splits bound bodies (watcher.hub_framing)
         self.core = native.load().ReaderHub(max(64 * 1024, int(buf_bytes)), max(2, int(nbufs)),
                                             max(0, int(max_bytes)), frame=bool(frame))
-        # recv_slice: bytes per recv() call, each framed while in the reader's
-        # L2 (watcher.watch_recv_slice; 0: one recv per buffer)
-        if recv_slice:
-            self.core.set_recv_slice(int(recv_slice))
         # depth: buffers read ahead per stream (watcher.watch_reader_depth)
         if depth != 2:
             self.core.set_depth(int(depth))
-        # frame_defer: a reader behind its socket leaves framing to the loop's
-        # take until it has caught up (watcher.hub_frame_defer)
-        mode = {"off": 0, "caught_up": 1, "per_read": 2}[frame_defer]
-        if mode:
-            self.core.set_frame_defer(mode)
         self.protos: Dict[int, object] = {}
         self._tls: Dict[tuple, object] = {}
         self._flush: Dict[object, object] = {}  # bind(): once per dispatch

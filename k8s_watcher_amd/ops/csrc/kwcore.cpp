@@ -1897,34 +1897,6 @@ PyTypeObject ScannerType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 // step — rvs[i] as ndigits zero-padded decimal digits at buf[rv_off[i]], and
 // uid_text at every buf[uid_off[j]] — bounds-checked, in place. The numpy
 // version of this was most of the fixture's time at ~1.5M events/s.
-// touch_lines(buffer) -> int: read one word of every 64-byte line of a
-// buffer (no GIL), pulling it into this core's caches and the shared L3. The
-// replay fixture runs it on each slice of its zero-copy ring just before
-// sendfile()ing it: the watcher's recv() then copies from cache instead of
-// DRAM (testing/cluster_replay.py, ZeroCopyRing). Returns a checksum so the
-// reads are not elided.
-PyObject* kw_touch_lines(PyObject*, PyObject* arg) {
-    Py_buffer v;
-    if (PyObject_GetBuffer(arg, &v, PyBUF_SIMPLE) < 0) return nullptr;
-    uint64_t sum = 0;
-    const char* p = (const char*)v.buf;
-    const size_t n = (size_t)v.len;
-    Py_BEGIN_ALLOW_THREADS
-    size_t i = 0;
-    for (; i + 256 <= n; i += 256) {  // four lines per round: several misses in flight
-        uint64_t a, b, c, d;
-        std::memcpy(&a, p + i, 8);
-        std::memcpy(&b, p + i + 64, 8);
-        std::memcpy(&c, p + i + 128, 8);
-        std::memcpy(&d, p + i + 192, 8);
-        sum += a ^ b ^ c ^ d;
-    }
-    for (; i < n; i += 64) sum += (unsigned char)p[i];
-    Py_END_ALLOW_THREADS
-    PyBuffer_Release(&v);
-    return PyLong_FromUnsignedLongLong(sum);
-}
-
 PyObject* kw_stamp_fields(PyObject*, PyObject* args) {
     Py_buffer buf, rvo, rvs, uo;
     int nd;
@@ -2138,8 +2110,6 @@ PyMethodDef module_methods[] = {
     {"bench_validate", (PyCFunction)kw_bench_validate, METH_VARARGS, "bench_validate(lines, repeat) -> (seconds, invalid)"},
     {"bench_parse", (PyCFunction)kw_bench_parse, METH_VARARGS, "bench_parse(data, mode=2, repeat=1)"},
     {"event_timestamp", (PyCFunction)kw_event_timestamp, METH_O, "event_timestamp(utc) -> str"},
-    {"touch_lines", (PyCFunction)kw_touch_lines, METH_O,
-     "touch_lines(buffer) -> checksum: read one word per 64-byte line (warm the caches before a sendfile)"},
     {"stamp_fields", (PyCFunction)kw_stamp_fields, METH_VARARGS,
      "stamp_fields(buf, rv_off, rvs, ndigits, uid_off, uid_text): fixture re-stamping (int64 arrays)"},
     {"cpu_features", (PyCFunction)kw_cpu_features, METH_NOARGS, "SIMD paths in use"},

@@ -66,9 +66,8 @@ from .podgen import PodFactory
 try:  # the watcher's native module also re-stamps fixture buffers (optional here)
     from ..ops.native import load as _load_native
     _stamp = _load_native().stamp_fields
-    _touch = getattr(_load_native(), "touch_lines", None)
 except Exception:  # noqa: BLE001 - fixtures must run without the extension too
-    _stamp = _touch = None
+    _stamp = None
 
 RV0 = 1_000_000_000  # every resourceVersion has exactly 10 digits (room for 180k steps of 50k events)
 RV_DIGITS = 10
@@ -401,12 +400,11 @@ class Worker:
     """One serving process: its share of the watch connections, every command."""
 
     def __init__(self, model: ClusterModel, sock: socket.socket, slice_bytes: int = 1 << 20,
-                 zero_copy: bool = True, warm: bool = False) -> None:
+                 zero_copy: bool = True) -> None:
         self.m = model
         self.sock = sock
         self.slice = slice_bytes
         self.zero_copy = zero_copy
-        self.warm = warm
         self.rq_bound = receive_queue_bound() + (1 << 20)
         self.rings: Dict[str, ZeroCopyRing] = {}
         self.scopes: Dict[str, ScopeStream] = {}
@@ -570,27 +568,14 @@ class Worker:
         return r
 
     async def _send_zc(self, w: asyncio.StreamWriter, sc: ScopeStream, ring: ZeroCopyRing, k: int) -> None:
-        """sendfile the step from its ring slot, slice by slice; with
-        ``warm`` each slice is first read through once (``touch_lines``): the
-        pages were last touched three steps ago and are in DRAM, and the
-        watcher's recv() copying them cold cost its reader thread ~0.4 core at
-        2.3M events/s on the MI355X host (profiles/r4). Warm, they are in the
-        L3 the fixture shares with the watcher (bench --fixture-placement
-        inherit), as a NIC's DMA into the last-level cache would leave them."""
+        """sendfile the step from its ring slot."""
         loop = asyncio.get_running_loop()
         try:
             i = await ring.slot_for(sc, k)
             sock = w.get_extra_info("socket")
             raw = getattr(sock, "_sock", sock)  # asyncio's TransportSocket wraps the socket
             base = i * ring.n
-            if self.warm and _touch is not None:
-                view = ring.views[i]
-                for off in range(0, ring.n, self.slice):
-                    end = min(ring.n, off + self.slice)
-                    _touch(view[off:end])
-                    await loop.sendfile(w.transport, ring.file, base + off, end - off, fallback=False)
-            else:
-                await loop.sendfile(w.transport, ring.file, base, ring.n, fallback=False)
+            await loop.sendfile(w.transport, ring.file, base, ring.n, fallback=False)
             ring.bytes += ring.n
             ring.note_sent(i, raw)
         except (ConnectionError, RuntimeError, OSError):
@@ -739,8 +724,7 @@ def run(args) -> None:
                         ssl_ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
                         ssl_ctx.load_cert_chain(args.tls_cert, args.tls_key)
                     asyncio.run(Worker(model, _reuseport_socket(ports[g], listen=True),
-                                       zero_copy=args.zero_copy != "off",
-                                       warm=args.zero_copy == "warm").serve(c_r, r_w, ssl_ctx))
+                                       zero_copy=args.zero_copy != "off").serve(c_r, r_w, ssl_ctx))
                 finally:
                     os._exit(0)
             os.close(c_r)
@@ -804,11 +788,9 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--notify", default="critical", choices=["critical", "all"],
                     help="which events of the target namespaces count as notifiable: the production "
                          "profile's critical-events filter, or every one (development/staging)")
-    ap.add_argument("--zero-copy", default="auto", choices=["auto", "warm", "off"],
+    ap.add_argument("--zero-copy", default="auto", choices=["auto", "off"],
                     help="auto: scopes whose step outgrows a peer's receive buffer are sent with sendfile "
-                         "from a memfd ring (ZeroCopyRing); warm: each slice is read through first so it "
-                         "leaves from cache (moves ~0.45 core of the receiver's cold copy to the fixture, "
-                         "profiles/r4/zero_copy_gpu_box.md); off: every scope is written (copied)")
+                         "from a memfd ring (ZeroCopyRing); off: every scope is written (copied)")
     ap.add_argument("--prototypes", type=int, default=256)
     ap.add_argument("--seed", type=int, default=0)
     run(ap.parse_args(argv))

@@ -174,13 +174,6 @@ def _as_int(value: Any, key: str) -> int:
     return out
 
 
-def _recv_slice(value: Any) -> int:
-    n = _as_int(value, "watcher.watch_recv_slice")
-    if n < 0 or 0 < n < 4096:
-        raise ConfigError(f"watcher.watch_recv_slice: 0 or at least 4096 bytes, got {n}")
-    return n
-
-
 def _reader_depth(value: Any) -> int:
     n = _as_int(value, "watcher.watch_reader_depth")
     if not 2 <= n <= 8:
@@ -321,13 +314,7 @@ class WatcherSettings:
     watch_reader: str = "native"  # native (ReaderHub thread, plain TCP + native engine) | asyncio
     watch_reader_buffers: int = 64  # ReaderHub pool: up to this many buffers of watch_read_bytes (allocated on use)
     watch_reader_max_bytes: int = 0  # ReaderHub read-ahead over all streams (0: the whole pool)
-    watch_recv_slice: int = 0  # ReaderHub bytes per recv() call, framed in L2 (0: one recv per buffer)
     watch_reader_depth: int = 2  # ReaderHub read-ahead per stream, in buffers (2..8)
-    # a reader thread behind its socket (a read filled its buffer) leaves the
-    # framing of that stream to the event loop's take until it has caught up
-    # (off | caught_up: until the loop has caught up | per_read: each read
-    # that fills its buffer on its own)
-    hub_frame_defer: str = "off"
     hub_dispatch: bool = True  # hub-read watches feed the native pipeline with no Python call per read
     hub_framing: bool = True  # ... and the hub's thread de-chunks and splits their bodies (readerhub.inc HubFramer)
     partitioned_apply: bool = True  # a batch's apply split by pod-cache shard over the decode pool (engine.inc)
@@ -519,10 +506,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         watch_reader=_choice(w.get("watch_reader", "native"), "watcher.watch_reader", ("native", "asyncio")),
         watch_reader_buffers=max(2, _as_int(w.get("watch_reader_buffers", 64), "watcher.watch_reader_buffers")),
         watch_reader_max_bytes=max(0, _as_int(w.get("watch_reader_max_bytes", 0), "watcher.watch_reader_max_bytes")),
-        watch_recv_slice=_recv_slice(w.get("watch_recv_slice", 0)),
         watch_reader_depth=_reader_depth(w.get("watch_reader_depth", 2)),
-        hub_frame_defer=_choice(w.get("hub_frame_defer", "off"), "watcher.hub_frame_defer",
-                                ("off", "caught_up", "per_read")),
         hub_dispatch=_as_bool(w.get("hub_dispatch", True), "watcher.hub_dispatch"),
         hub_framing=_as_bool(w.get("hub_framing", True), "watcher.hub_framing"),
         partitioned_apply=_as_bool(w.get("partitioned_apply", True), "watcher.partitioned_apply"),

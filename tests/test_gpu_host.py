@@ -74,8 +74,8 @@ def test_hub_framing_and_grouped_dispatch_on_host():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import test_reader_hub
     for seed in (1, 2, 3):
-        for recv_slice in (0, 4096, 5000, "defer", "defer_per_read"):
-            test_reader_hub.test_hub_framing_matches_pipeline_framing_on_random_chunking(seed, recv_slice)
+        for buf_bytes in (16 * 1024, 64 * 1024):
+            test_reader_hub.test_hub_framing_matches_pipeline_framing_on_random_chunking(seed, buf_bytes)
     test_reader_hub.test_take_dispatch_groups_many_bound_streams_like_serial_feeding()
     test_reader_hub.test_busy_streams_grow_only_to_their_share_of_the_pool()
     line = run_bench(["--steps", "2", "--warmup", "1",

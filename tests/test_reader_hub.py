@@ -567,19 +567,14 @@ def test_busy_streams_grow_only_to_their_share_of_the_pool():
         b.close()
 
 
-@pytest.mark.parametrize("recv_slice", [0, 4096, 5000, "defer", "defer_per_read"])
+@pytest.mark.parametrize("buf_bytes", [16 * 1024, 64 * 1024])
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_hub_framing_matches_pipeline_framing_on_random_chunking(seed, recv_slice):
+def test_hub_framing_matches_pipeline_framing_on_random_chunking(seed, buf_bytes):
     """Once a chunked body is bound, the hub frames it (chunk de-framing and
     line splitting on its reader thread, HubFramer) and the pipeline walks
     line items: random chunk sizes, random send pieces and small buffers put
     chunk headers, line ends and buffer ends everywhere — the result is
-    identical to the pipeline framing the same bytes itself. With a recv
-    slice (watcher.watch_recv_slice) each recv() of a buffer is framed on its
-    own, so slice ends land everywhere too. "defer": whole-buffer reads with
-    watcher.hub_frame_defer — a read that fills its small buffer leaves the
-    stream's framing to take() until it has caught up, so the framing moves
-    between the reader thread and the consumer mid-stream, repeatedly."""
+    identical to the pipeline framing the same bytes itself."""
     import random
     import threading
     from test_native_pipeline import Recorder, run_native, stream
@@ -604,12 +599,7 @@ def test_hub_framing_matches_pipeline_framing_on_random_chunking(seed, recv_slic
     p.log_events_setting = False
     p.attach_native(load().DecodePool(2))
     p.sync_native_log()
-    core = load().ReaderHub(16 * 1024, 16)
-    defer = {"defer": 1, "defer_per_read": 2}.get(recv_slice, 0)
-    recv_slice = 0 if defer else recv_slice
-    core.set_recv_slice(recv_slice)
-    core.set_frame_defer(defer)
-    assert core.stats()["recv_slice"] == recv_slice and core.stats()["frame_defer"] == defer
+    core = load().ReaderHub(buf_bytes, 16)
     a, b = socket.socketpair()
     sid = core.add(os.dup(b.fileno()))
     core.bind(sid, p.native, True)
@@ -645,28 +635,18 @@ def test_hub_framing_matches_pipeline_framing_on_random_chunking(seed, recv_slic
     st = core.stats()
     assert st["framed_reads"] > 0 and st["frame_ns"] > 0  # the hub did frame (after the first take)
     assert st["recv_bytes"] == len(raw) and st["recv_ns"] > 0
-    if defer:  # the reader fell behind and handed framing over, and the consumer framed
-        assert st["deferred_reads"] > 0 and st["consumer_frame_ns"] > 0
     core.close()
     a.close()
     b.close()
 
 
-def test_recv_slice_setting():
+def test_reader_depth_setting():
     from k8s_watcher_amd.utils.config import ConfigError, load_settings
-    assert load_settings("production", environ={}).watcher.watch_recv_slice == 0
-    s = load_settings("production", overrides={"watcher": {"watch_recv_slice": 262144}}, environ={})
-    assert s.watcher.watch_recv_slice == 262144
-    for bad in (-1, 100):
-        with pytest.raises(ConfigError):
-            load_settings("production", overrides={"watcher": {"watch_recv_slice": bad}}, environ={})
     assert load_settings("production", environ={}).watcher.watch_reader_depth == 2
     for bad in (1, 9):
         with pytest.raises(ConfigError):
             load_settings("production", overrides={"watcher": {"watch_reader_depth": bad}}, environ={})
     core = load().ReaderHub(16 * 1024, 4)
-    with pytest.raises(ValueError):
-        core.set_recv_slice(100)
     with pytest.raises(ValueError):
         core.set_depth(9)
     core.set_depth(4)
