@@ -36,11 +36,11 @@ from ..kube.api import ApiError, KubeApi
 from ..kube.kubeconfig import ConfigException, KubeEndpoint, load_incluster_config, load_kube_config
 from ..metrics import Metrics, start_metrics_server
 from ..net.http import HttpError
-from ..ops.cache import make_pod_cache
+from ..ops.cache import CORE, NAME, NS, PHASE, RV, make_pod_cache
 from ..ops.decode import make_decoder
 from ..parallel.native_notifier import NativeNotifierPool
 from ..parallel.notifier import NotifierPool, NullNotifier
-from ..parallel.shard import ShardFilter
+from ..parallel.shard import ShardFilter, owner_of, take_handover, write_handover
 from ..parallel.spool import Spool, SpoolReplayer
 from ..utils.config import Settings
 from ..utils.fastlog import EventLog
@@ -110,6 +110,10 @@ class WatcherService:
         self.spool_replayer = None
         self.ns_watcher: Optional[NamespaceWatcher] = None
         self._scope_tasks: Dict[str, asyncio.Task] = {}
+        # namespaces gained from another shard, waiting for its hand-over record
+        # before their watch starts (watcher.shard.handover_dir)
+        self._gaining: Dict[str, asyncio.Task] = {}
+        self._ns_seen: Set[str] = set()  # the namespace set the last ownership decision used
         self._retiring: Dict[str, asyncio.TimerHandle] = {}  # deleted namespaces draining their pod watch
         self._failure: Optional[asyncio.Future] = None
         self._saved_rvs: Dict[str, Optional[str]] = {}
@@ -274,7 +278,8 @@ class WatcherService:
                 if ns_task.exception() is not None:
                     raise ns_task.exception()  # type: ignore[misc]
                 raise SetupError("namespace watch ended before the initial list")
-            scopes: List[Optional[str]] = list(self._owned(self.ns_watcher.names))
+            self._ns_seen = set(self.ns_watcher.names)
+            scopes: List[Optional[str]] = list(self._owned(self._ns_seen))
         elif scope_mode == "server" and s.watcher.namespaces:
             scopes = list(ShardFilter(s.watcher.shard).namespaces(s.watcher.namespaces))
         else:
@@ -429,17 +434,75 @@ class WatcherService:
         if exc is not None and self._failure is not None and not self._failure.done():
             self._failure.set_exception(exc)
 
-    def _stop_scope(self, ns: str) -> None:
+    def _stop_scope(self, ns: str, handover_to: Optional[int] = None) -> None:
         timer = self._retiring.pop(ns, None)
         if timer is not None:
             timer.cancel()
+        gaining = self._gaining.pop(ns, None)
+        if gaining is not None:  # handed on before its watch started: nothing of it is cached here
+            gaining.cancel()
         task = self._scope_tasks.pop(ns, None)
-        for r in [r for r in self.reflectors if r.namespace == ns]:
+        stopped = [r for r in self.reflectors if r.namespace == ns]
+        for r in stopped:
             r.stop()
             self.reflectors.remove(r)
         if task is not None and not task.done():
             task.cancel()
+        if handover_to is not None and stopped:
+            self._handover_out(ns, handover_to)
         self._forget_namespaces({ns})
+
+    def _handover_out(self, ns: str, dst: int) -> None:
+        """The old owner's half of a namespace hand-over: with its watch
+        stopped, this shard's cached pods of ``ns`` go to the shared
+        directory for shard ``dst`` (parallel/shard.py)."""
+        sh = self.settings.watcher.shard
+        cache = self.pipeline.cache if self.pipeline is not None else None
+        if cache is None:
+            return
+        pods = [(uid, e[RV], e[PHASE], e[NAME], e[CORE]) for uid, e in cache.items() if e[NS] == ns]
+        try:
+            write_handover(sh.handover_dir, ns, sh.index, dst, pods)
+        except OSError as exc:
+            self.metrics.c["shard_handover_errors"] += 1
+            self.log.error(f"Could not write the hand-over of namespace {ns} to shard {dst} "
+                           f"({exc}): its new owner will re-announce its pods")
+            return
+        self.metrics.c["shard_handovers_out"] += 1
+        self.metrics.c["shard_handover_pods_out"] += len(pods)
+        self.log.info(f"Handed namespace {ns} ({len(pods)} cached pods) over to shard {dst}")
+
+    def _gain_scope(self, ns: str) -> None:
+        self._gaining[ns] = asyncio.ensure_future(self._await_handover(ns))
+
+    async def _await_handover(self, ns: str) -> None:
+        """The new owner's half: wait for the old owner's record, load it into
+        the cache, then start the watch — its first LIST reconciles against
+        that state (unchanged pods stay quiet, pods gone meanwhile are
+        DELETED), as a relist after a 410 would."""
+        sh = self.settings.watcher.shard
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + sh.handover_wait_seconds
+        while True:
+            pods = take_handover(sh.handover_dir, ns, sh.index)
+            if pods is not None or loop.time() >= deadline or self._stop.is_set():
+                break
+            await asyncio.sleep(0.05)
+        if self._gaining.get(ns) is not asyncio.current_task() or self._stop.is_set():
+            return
+        del self._gaining[ns]
+        if pods is None:
+            self.metrics.c["shard_handover_timeouts"] += 1
+            self.log.warning(f"No hand-over of namespace {ns} from its old owner after "
+                             f"{sh.handover_wait_seconds}s: its pods are announced as ADDED again")
+        else:
+            cache = self.pipeline.cache
+            for uid, rv, phase, name, core in pods:
+                cache.put(uid, rv, phase, ns, name, core)
+            self.metrics.c["shard_handovers_in"] += 1
+            self.metrics.c["shard_handover_pods_in"] += len(pods)
+            self.log.info(f"Took over namespace {ns} ({len(pods)} pods from its old owner)")
+        self._start_scope(ns, primed=True)
 
     def _forget_namespaces(self, namespaces: Set[str]) -> None:
         """Drop cached pods of namespaces this shard stopped watching, silently:
@@ -478,22 +541,30 @@ class WatcherService:
         deletes the pods before the namespace, but nothing orders two streams)."""
         if not self._live or self._stop.is_set():
             return
+        sh = self.settings.watcher.shard
+        prev, self._ns_seen = self._ns_seen, set(names)
         owned = set(self._owned(names))
-        current = set(self._scope_tasks)
+        current = set(self._scope_tasks) | set(self._gaining)
         for ns in sorted(owned & set(self._retiring)):  # deleted and created again: keep watching
             self._retiring.pop(ns).cancel()
         for ns in sorted(owned - current):
             self.metrics.c["scopes_started"] += 1
-            self.log.info(f"Watching namespace {ns} (new or now owned by shard {self.settings.watcher.shard.index})")
-            self._start_scope(ns, primed=True)
+            self.log.info(f"Watching namespace {ns} (new or now owned by shard {sh.index})")
+            if sh.handover_dir and ns in prev and owner_of(ns, prev, sh.count, sh.assignment) != sh.index:
+                self._gain_scope(ns)  # moved here from another shard: its state first
+            else:
+                self._start_scope(ns, primed=True)
         for ns in sorted(current - owned):
+            if ns in self._gaining and ns not in names:  # deleted before its hand-over came
+                self._gaining.pop(ns).cancel()
+                continue
             if ns not in names:
                 if ns not in self._retiring:  # already draining: its timer is running
                     self._retire_scope(ns)
                 continue
             self.metrics.c["scopes_stopped"] += 1
             self.log.info(f"Stopped watching namespace {ns} (owned by another shard)")
-            self._stop_scope(ns)
+            self._stop_scope(ns, owner_of(ns, names, sh.count, sh.assignment) if sh.handover_dir else None)
 
     def _cached_in(self, ns: str) -> int:
         cache = self.pipeline.cache if self.pipeline is not None else None
@@ -680,7 +751,7 @@ class WatcherService:
             # it land first, so the final cut is the one that stays on disk
             await self._await_inflight_checkpoint()
             await self._write_checkpoint()  # format 2 carries whatever is still owed
-        tasks = list(self._tasks) + list(self._scope_tasks.values())
+        tasks = list(self._tasks) + list(self._scope_tasks.values()) + list(self._gaining.values())
         for t in tasks:
             if not t.done():
                 t.cancel()

@@ -62,6 +62,12 @@ COUNTERS = (
     "namespace_changes",    # namespace set changes seen by watcher.namespace_scope: discover
     "scopes_started",       # per-namespace pod watches opened after start-up (new or handed-over namespaces)
     "scopes_stopped",       # ... and closed (namespace deleted or now owned by another shard)
+    "shard_handovers_out",  # namespaces handed to another shard with their cached pods (shard.handover_dir)
+    "shard_handover_pods_out",
+    "shard_handovers_in",   # ... taken over from another shard's record
+    "shard_handover_pods_in",
+    "shard_handover_timeouts",  # a moved namespace's record never came (its pods re-announced)
+    "shard_handover_errors",    # a record could not be written
     "notify_io_switches",   # clusterapi.pool.io_thread: auto — sockets handed between loop and I/O thread
     "namespace_deleted_synthesized",  # pods of a deleted namespace notified DELETED from the cache (no event came)
     "leader_acquired",      # leadership terms started (engine/leader.py)

@@ -26,13 +26,18 @@ Two ways to decide which shard owns what:
     still has room under ``ceil(n / count)``, so every shard owns ``floor``
     or ``ceil`` of ``n / count`` namespaces. Meant for a fixed namespace
     set: when ``ceil(n / count)`` changes, a few namespaces move to another
-    shard, whose first LIST re-announces their pods as ``ADDED``
-    (at-least-once for pods that exist across that hand-over). Deletions
-    are not covered: the losing shard forgets the namespace's cached pods
-    without notifying, and the gaining shard's LIST only sees pods that
-    still exist, so a pod deleted between the two shards' views of the
-    namespace set is never reported ``DELETED``. Use ``hash`` (namespaces
-    never move) where every deletion must be reported.
+    shard.
+
+A namespace that moves (``balanced`` on a namespace-set change) is handed
+over when ``shard.handover_dir`` names a directory all shards share: the
+old owner stops its watch, then writes its cached pods of the namespace
+there (:func:`write_handover`, one JSON file, atomically renamed); the new
+owner waits for that record (``shard.handover_wait_seconds``), loads it into
+its cache and only then LISTs — so pods that stayed are not re-announced and
+a pod deleted while neither shard watched is reported ``DELETED`` by the new
+owner's reconcile, exactly once. Without the directory (or if the old owner
+is gone and the wait runs out) the new owner's LIST re-announces the pods as
+``ADDED`` (at-least-once) and a deletion inside that window is not reported.
 
 crc32 is stable across processes and Python versions, unlike ``hash()``.
 """
@@ -40,8 +45,11 @@ crc32 is stable across processes and Python versions, unlike ``hash()``.
 from __future__ import annotations
 
 import bisect
+import json
+import os
+import tempfile
 import zlib
-from typing import Dict, Iterable, List, Optional, Sequence
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 from ..utils.config import ShardSettings
 
@@ -79,6 +87,68 @@ def balanced_assignment(names: Iterable[str], count: int) -> Dict[str, int]:
         load[s] += 1
         out[name] = s
     return out
+
+
+def owner_of(namespace: str, names: Iterable[str], count: int, assignment: str) -> int:
+    """The shard owning ``namespace`` when the namespace set is ``names``."""
+    if count <= 1:
+        return 0
+    if assignment == "hash":
+        return shard_of(namespace, count)
+    return balanced_assignment(list(names) + [namespace], count).get(namespace, 0)
+
+
+# ---------------------------------------------------------------- hand-over
+HANDOVER_VERSION = 1
+
+
+def _handover_path(directory: str, namespace: str) -> str:
+    return os.path.join(directory, f"{namespace}.handover.json")
+
+
+def write_handover(directory: str, namespace: str, src: int, dst: int,
+                   pods: List[Tuple[str, Optional[str], Optional[str], Optional[str], Optional[bytes]]]) -> str:
+    """The old owner's cached pods of ``namespace`` — ``(uid, rv, phase, name,
+    core)`` — for shard ``dst``; written to a temporary name and renamed, so a
+    reader sees the whole record or none."""
+    os.makedirs(directory, exist_ok=True)
+    doc = {"version": HANDOVER_VERSION, "namespace": namespace, "from": src, "to": dst,
+           "pods": [[u, rv, ph, nm, core.decode("utf-8", "replace") if core is not None else None]
+                    for u, rv, ph, nm, core in pods]}
+    path = _handover_path(directory, namespace)
+    fd, tmp = tempfile.mkstemp(prefix=f".{namespace}.", dir=directory)
+    try:
+        with os.fdopen(fd, "w") as f:
+            json.dump(doc, f, separators=(",", ":"))
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, path)
+    except BaseException:
+        try:
+            os.unlink(tmp)
+        except OSError:
+            pass
+        raise
+    return path
+
+
+def take_handover(directory: str, namespace: str, dst: int):
+    """The record for shard ``dst`` if one is there (consumed: the file is
+    removed), else None. Records addressed to another shard are left alone."""
+    path = _handover_path(directory, namespace)
+    try:
+        with open(path) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if doc.get("version") != HANDOVER_VERSION or doc.get("namespace") != namespace or doc.get("to") != dst:
+        return None
+    try:
+        os.unlink(path)
+    except OSError:
+        pass
+    return [(u, rv, ph, nm, core.encode("utf-8") if core is not None else None)
+            for u, rv, ph, nm, core in doc.get("pods", [])]
 
 
 class ShardFilter:

@@ -363,6 +363,13 @@ class ShardSettings:
     index: int = 0
     key: str = "namespace"  # namespace | uid
     assignment: str = "hash"  # hash | balanced: namespace -> shard for per-namespace watches (parallel/shard.py)
+    # a directory every shard can read and write (a shared volume): a shard
+    # handing a namespace to another writes its cached pods there, and the new
+    # owner's first LIST reconciles against them — no re-ADDED for pods that
+    # stayed, DELETED for pods gone in between ("" = off: at-least-once ADDED,
+    # deletions during a hand-over unreported; parallel/shard.py)
+    handover_dir: str = ""
+    handover_wait_seconds: float = 10.0  # the new owner waits this long for the old owner's record
 
 
 @dataclass
@@ -400,7 +407,10 @@ def _shard(block: Dict[str, Any]) -> ShardSettings:
     s = ShardSettings(count=_as_int(count, "watcher.shard.count"), index=_as_int(index, "watcher.shard.index"),
                       key=_choice(block.get("key", "namespace"), "watcher.shard.key", ("namespace", "uid")),
                       assignment=_choice(block.get("assignment", "hash"), "watcher.shard.assignment",
-                                         ("balanced", "hash")))
+                                         ("balanced", "hash")),
+                      handover_dir=str(block.get("handover_dir") or ""),
+                      handover_wait_seconds=_bounded_float(block.get("handover_wait_seconds", 10.0),
+                                                           "watcher.shard.handover_wait_seconds", 0.0, 3600.0))
     if s.count < 1 or not 0 <= s.index < s.count:
         raise ConfigError(f"watcher.shard: index {s.index} outside [0, {s.count})")
     return s

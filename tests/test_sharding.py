@@ -528,3 +528,89 @@ def test_restart_owed_modified_then_deleted_namespace_ends_deleted(tmp_path):
     mine, owed_resent = run(body(), timeout=60)
     assert owed_resent == 1
     assert mine == ["ADDED", "MODIFIED", "DELETED"], mine
+
+
+def test_handover_record_roundtrip(tmp_path):
+    from k8s_watcher_amd.parallel.shard import take_handover, write_handover
+    pods = [("u1", "10", "Running", "a", b'{"x":1'), ("u2", None, None, "b", None)]
+    write_handover(str(tmp_path), "ns-a", 0, 1, pods)
+    assert take_handover(str(tmp_path), "ns-a", 0) is None  # addressed to shard 1: left alone
+    assert take_handover(str(tmp_path), "ns-a", 1) == pods
+    assert take_handover(str(tmp_path), "ns-a", 1) is None  # consumed
+    assert not [f for f in os.listdir(tmp_path)]  # no temporary file left behind
+
+
+@pytest.mark.parametrize("engine", ["native", "python"])
+def test_balanced_move_hands_over_state_and_reports_deletion_exactly_once(tmp_path, engine):
+    """``balanced`` moves a namespace when the namespace set grows. With
+    ``shard.handover_dir`` the old owner writes its cached pods there and the
+    new owner's first LIST reconciles against them: the moved namespace's pods
+    are not re-announced, and a pod deleted while neither shard watched it
+    (here: removed from the API server without a watch event, so only the
+    reconcile can find out) is reported DELETED exactly once — the deletion
+    hole ``balanced`` had without a hand-over."""
+    from k8s_watcher_amd.engine.service import WatcherService
+    from k8s_watcher_amd.kube.kubeconfig import KubeEndpoint
+    from k8s_watcher_amd.metrics import Metrics
+    from k8s_watcher_amd.parallel.shard import balanced_assignment
+
+    nss = [f"ns-{i}" for i in range(10)]
+    before = balanced_assignment(nss, 2)
+    late, moved = None, []
+    for i in range(200):  # a new namespace whose arrival moves some of the others
+        cand = f"late-{i}"
+        after = balanced_assignment(nss + [cand], 2)
+        moved = [n for n in nss if before[n] != after[n]]
+        if moved:
+            late = cand
+            break
+    assert late is not None
+
+    async def body():
+        srv = FakeApiServer(namespaces=nss)
+        await srv.start()
+        sink = StubSink()
+        await sink.start()
+        svcs = []
+        for i in range(2):
+            s = load_settings("staging", overrides={
+                "clusterapi": {"base_url": sink.url, "health_check_on_start": False},
+                "watcher": {"engine": engine, "namespace_scope": "discover",
+                            "shard": {"count": 2, "index": i, "assignment": "balanced",
+                                      "handover_dir": str(tmp_path), "handover_wait_seconds": 10},
+                            "retry": {"delay_seconds": 0.05, "max_attempts": 0}}})
+            svc = WatcherService(s, endpoint=KubeEndpoint(server=srv.url), metrics=Metrics())
+            await svc.start()
+            svcs.append(svc)
+        f = PodFactory(seed=6, namespaces=nss)
+        created = [srv.create(f.running(f.new_pod(namespace=nss[k % len(nss)]))) for k in range(40)]
+        await sink.state.wait_for(40, timeout=10)
+        await asyncio.sleep(0.2)
+        # a pod of a namespace about to move vanishes with no watch event
+        gone = next(p for p in created if p["metadata"]["namespace"] == moved[0])
+        del srv.pods[(moved[0], gone["metadata"]["name"])]
+        srv.add_namespace(late)
+        gainer = svcs[before[moved[0]] ^ 1]
+        for _ in range(200):
+            if gainer.metrics.c["shard_handovers_in"] >= len(moved) and \
+                    all(any(r.namespace == n and r.synced.is_set() for r in gainer.reflectors) for n in moved):
+                break
+            await asyncio.sleep(0.05)
+        await sink.state.wait_for(41, timeout=10)
+        await asyncio.sleep(0.3)
+        got = collections.Counter((p["uid"], p["event_type"]) for p in sink.state.payloads())
+        want = collections.Counter([(p["metadata"]["uid"], "ADDED") for p in created]
+                                   + [(gone["metadata"]["uid"], "DELETED")])
+        assert got == want
+        loser = svcs[before[moved[0]]]
+        assert loser.metrics.c["shard_handovers_out"] == len(moved) == gainer.metrics.c["shard_handovers_in"]
+        assert gainer.metrics.c["shard_handover_timeouts"] == 0
+        assert not any(r.namespace in moved for r in loser.reflectors)
+        assert not [x for x in os.listdir(tmp_path) if x.endswith(".handover.json")]  # all consumed
+        for svc in svcs:
+            svc.stop()
+            await svc.shutdown()
+        await sink.stop()
+        await srv.stop()
+
+    run(body(), timeout=60)
