@@ -316,11 +316,16 @@ class WatcherService:
                                                        or getattr(http.ssl_context, "kw_tls", None) is not None):
                 # watch bodies read (and, for https, decrypted) on a native thread (net/reader.py)
                 from ..net.reader import WatchReaderHub
+                from ..utils.cpus import auto_tls_threads
                 self._reader_hub = WatchReaderHub(s.watcher.watch_read_bytes or (4 << 20),
                                                   s.watcher.watch_reader_buffers,
                                                   max_bytes=s.watcher.watch_reader_max_bytes,
                                                   frame=s.watcher.hub_framing,
-                                                  depth=s.watcher.watch_reader_depth)
+                                                  depth=s.watcher.watch_reader_depth,
+                                                  tls_records=s.watcher.watch_tls_records == "native",
+                                                  tls_threads=(s.watcher.watch_tls_threads
+                                                               if s.watcher.watch_tls_threads >= 0
+                                                               else auto_tls_threads()))
                 self.api.http.reader_hub = self._reader_hub
                 hub = self._reader_hub
                 self.metrics.gauges["watch_reader_streams"] = lambda: float(len(hub.protos))

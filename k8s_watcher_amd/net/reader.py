@@ -38,7 +38,7 @@ class WatchReaderHub:
 
     def __init__(self, buf_bytes: int, nbufs: int = 64,
                  loop: Optional[asyncio.AbstractEventLoop] = None, max_bytes: int = 0, frame: bool = True,
-                 depth: int = 2) -> None:
+                 depth: int = 2, tls_records: bool = True, tls_threads: int = 0) -> None:
         self.loop = loop or asyncio.get_running_loop()
         # max_bytes: read-ahead over all streams (0: the whole pool); frame: the
         # hub's thread de-chunks and splits bound bodies (watcher.hub_framing)
@@ -47,6 +47,10 @@ class WatchReaderHub:
         # depth: buffers read ahead per stream (watcher.watch_reader_depth)
         if depth != 2:
             self.core.set_depth(int(depth))
+        # https watches: the hub opens TLS 1.3 records itself, on a pool of
+        # tls_threads besides the reader thread (watcher.watch_tls_records /
+        # watch_tls_threads; ops/csrc/tls13.inc)
+        self.core.set_tls(bool(tls_records), max(0, int(tls_threads)))
         self.protos: Dict[int, object] = {}
         self._tls: Dict[tuple, object] = {}
         self._flush: Dict[object, object] = {}  # bind(): once per dispatch

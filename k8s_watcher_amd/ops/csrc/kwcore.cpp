@@ -21,6 +21,8 @@
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <openssl/err.h>
+#include <openssl/evp.h>
+#include <openssl/hmac.h>
 #include <openssl/pem.h>
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
@@ -40,6 +42,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <array>
 #include <charconv>
 #include <atomic>
 #include <cctype>
@@ -50,6 +53,7 @@
 #include <cstring>
 #include <ctime>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -2043,6 +2047,7 @@ PyObject* kw_bench_parse(PyObject*, PyObject* args) {
 #include "engine.inc"
 #include "checkpoint.inc"
 #include "relist.inc"
+#include "tls13.inc"
 #include "readerhub.inc"
 #include "sinkserver.inc"
 #include "looplag.inc"
@@ -2150,7 +2155,7 @@ PyMODINIT_FUNC PyInit__kwcore(void) {
     Py_INCREF(&ScannerType);
     PyModule_AddObject(m, "ResponseScanner", (PyObject*)&ScannerType);
     if (register_engine(m) < 0 || register_podcache(m) < 0 || register_pipeline(m) < 0 || register_logsink(m) < 0 ||
-        register_checkpoint(m) < 0 || register_relist(m) < 0 || register_readerhub(m) < 0 || register_sinkserver(m) < 0 ||
+        register_checkpoint(m) < 0 || register_relist(m) < 0 || register_readerhub(m) < 0 || register_tls13(m) < 0 || register_sinkserver(m) < 0 ||
         register_looplag(m) < 0)
         return nullptr;
     const char* names[6] = {"ADDED", "MODIFIED", "DELETED", "BOOKMARK", "ERROR", "INVALID"};

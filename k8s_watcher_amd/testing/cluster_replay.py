@@ -50,6 +50,7 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import collections
 import json
 import os
 import random
@@ -633,9 +634,35 @@ class Worker:
             except ConnectionError:
                 pass
 
+    async def _accept_tls(self, tls) -> None:
+        """https with the native TLS server: accept, hand the socket to
+        OpenSSL for the handshake (on an executor thread), then serve the
+        connection through _TlsReader / _TlsWriter."""
+        import concurrent.futures
+        loop = asyncio.get_running_loop()
+        ex = concurrent.futures.ThreadPoolExecutor(max_workers=16, thread_name_prefix="tls")
+        self.sock.setblocking(False)
+
+        async def one(fd: int) -> None:
+            try:
+                conn = await loop.run_in_executor(ex, tls.accept, fd)
+            except OSError:
+                return
+            await self.handle(_TlsReader(conn), _TlsWriter(conn, ex))
+
+        while True:
+            c, _ = await loop.sock_accept(self.sock)
+            c.setblocking(False)
+            asyncio.ensure_future(one(c.detach()))
+
     async def serve(self, ctrl_in: int, ctrl_out: int, ssl_ctx=None) -> None:
         loop = asyncio.get_running_loop()
-        server = await asyncio.start_server(self.handle, sock=self.sock, limit=1 << 20, ssl=ssl_ctx)
+        if ssl_ctx is not None and not isinstance(ssl_ctx, __import__("ssl").SSLContext):
+            server = None  # native TLS (a _kwcore.TlsServerContext)
+            acceptor = asyncio.ensure_future(self._accept_tls(ssl_ctx))
+        else:
+            server = await asyncio.start_server(self.handle, sock=self.sock, limit=1 << 20, ssl=ssl_ctx)
+            acceptor = None
         reader = asyncio.StreamReader()
         await loop.connect_read_pipe(lambda: asyncio.StreamReaderProtocol(reader), os.fdopen(ctrl_in, "rb"))
         out = os.fdopen(ctrl_out, "wb", buffering=0)
@@ -664,9 +691,130 @@ class Worker:
                 reply = json.dumps({n: {"bytes": r.bytes, "waits": r.waits} for n, r in self.rings.items()},
                                    separators=(",", ":"))
             out.write(reply.encode() + b"\n")
-        server.close()
+        if server is not None:
+            server.close()
+        if acceptor is not None:
+            acceptor.cancel()
         for r in self.rings.values():
             r.close()
+
+
+class _TlsReader:
+    """StreamReader's ``readline``/``read`` over a native TLS connection
+    (``_kwcore.TlsConn``): requests are decrypted by OpenSSL on the event
+    loop's thread when the socket is readable (non-blocking)."""
+
+    def __init__(self, conn) -> None:
+        self.conn = conn
+        self.buf = bytearray()
+        self.eof = False
+
+    async def _fill(self) -> None:
+        loop = asyncio.get_running_loop()
+        while True:
+            data = self.conn.recv(65536)
+            if data is None:  # nothing yet: wait for the socket
+                fd = self.conn.fileno()
+                if fd < 0:
+                    self.eof = True
+                    return
+                fut = loop.create_future()
+                loop.add_reader(fd, lambda: fut.done() or fut.set_result(None))
+                try:
+                    await fut
+                finally:
+                    loop.remove_reader(fd)
+                continue
+            if not data:
+                self.eof = True
+            self.buf += data
+            return
+
+    async def readline(self) -> bytes:
+        while True:
+            i = self.buf.find(b"\n")
+            if i >= 0:
+                line = bytes(self.buf[:i + 1])
+                del self.buf[:i + 1]
+                return line
+            if self.eof:
+                line = bytes(self.buf)
+                self.buf.clear()
+                return line
+            await self._fill()
+
+    async def read(self) -> bytes:
+        while not self.eof:
+            await self._fill()
+        data = bytes(self.buf)
+        self.buf.clear()
+        return data
+
+
+class _TlsWriter:
+    """StreamWriter's ``write``/``drain`` over a native TLS connection: writes
+    queue in order and go out on an executor thread, sealed into TLS 1.3
+    records on the context's thread pool (``_kwcore.TlsServerContext``) —
+    the event loop never encrypts. A queued view must stay unchanged until
+    ``drain()`` returns, as with the plain path's slices."""
+
+    def __init__(self, conn, executor) -> None:
+        self.conn = conn
+        self.ex = executor
+        self.q: "collections.deque" = collections.deque()
+        self.task = None
+        self.idle = asyncio.Event()
+        self.idle.set()
+        self.closed = False
+        self.failed = False
+
+    def write(self, data) -> None:
+        if self.closed:
+            return
+        self.q.append(data)
+        self.idle.clear()
+        if self.task is None:
+            self.task = asyncio.ensure_future(self._pump())
+
+    async def _pump(self) -> None:
+        loop = asyncio.get_running_loop()
+        try:
+            while self.q:
+                parts = [self.q.popleft()]
+                size = len(parts[0])
+                while self.q and size + len(self.q[0]) <= (1 << 20):  # small pieces go out together
+                    size += len(self.q[0])
+                    parts.append(self.q.popleft())
+                data = parts[0] if len(parts) == 1 else b"".join(parts)
+                await loop.run_in_executor(self.ex, self.conn.send, data)
+        except OSError:
+            self.failed = self.closed = True
+            self.q.clear()
+        finally:
+            self.task = None
+            self.idle.set()
+
+    async def drain(self) -> None:
+        await self.idle.wait()
+        if self.failed:
+            raise ConnectionResetError("TLS connection closed")
+
+    def is_closing(self) -> bool:
+        return self.closed
+
+    def get_extra_info(self, name: str, default=None):
+        return True if name == "sslcontext" else default
+
+    def close(self) -> None:
+        if self.conn is None:
+            return
+        self.closed = True
+        conn, self.conn = self.conn, None
+
+        async def later() -> None:
+            await self.idle.wait()
+            conn.close()
+        asyncio.ensure_future(later())
 
 
 def _cpu_list(text: str) -> set:
@@ -720,9 +868,13 @@ def run(args) -> None:
                         os.sched_setaffinity(0, cpus[g])
                     ssl_ctx = None
                     if args.tls_cert:  # https API server (the watcher's TLS path)
-                        import ssl
-                        ssl_ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
-                        ssl_ctx.load_cert_chain(args.tls_cert, args.tls_key)
+                        if args.tls_engine == "native":  # records sealed on a thread pool (ops/csrc/tls13.inc)
+                            ssl_ctx = _load_native().TlsServerContext(args.tls_cert, args.tls_key,
+                                                                      threads=args.tls_threads)
+                        else:
+                            import ssl
+                            ssl_ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+                            ssl_ctx.load_cert_chain(args.tls_cert, args.tls_key)
                     asyncio.run(Worker(model, _reuseport_socket(ports[g], listen=True),
                                        zero_copy=args.zero_copy != "off").serve(c_r, r_w, ssl_ctx))
                 finally:
@@ -784,6 +936,10 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--groups", type=int, default=1, help="front-ends (ports) serving the same cluster")
     ap.add_argument("--tls-cert", default=None, help="serve https with this certificate (and --tls-key)")
     ap.add_argument("--tls-key", default=None)
+    ap.add_argument("--tls-engine", default="native", choices=["native", "python"],
+                    help="native: OpenSSL handshake + TLS 1.3 records sealed on --tls-threads threads "
+                         "(_kwcore.TlsServerContext); python: asyncio's ssl transport")
+    ap.add_argument("--tls-threads", type=int, default=3, help="sealing threads per worker (native TLS)")
     ap.add_argument("--group-cpus", default=None, help="';'-separated CPU lists, one per front-end")
     ap.add_argument("--notify", default="critical", choices=["critical", "all"],
                     help="which events of the target namespaces count as notifiable: the production "

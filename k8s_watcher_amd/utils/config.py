@@ -174,6 +174,13 @@ def _as_int(value: Any, key: str) -> int:
     return out
 
 
+def _bounded_int(value: Any, key: str, lo: int, hi: int) -> int:
+    n = _as_int(value, key)
+    if not lo <= n <= hi:
+        raise ConfigError(f"{key}: {lo}..{hi}, got {n}")
+    return n
+
+
 def _reader_depth(value: Any) -> int:
     n = _as_int(value, "watcher.watch_reader_depth")
     if not 2 <= n <= 8:
@@ -315,6 +322,11 @@ class WatcherSettings:
     watch_reader_buffers: int = 64  # ReaderHub pool: up to this many buffers of watch_read_bytes (allocated on use)
     watch_reader_max_bytes: int = 0  # ReaderHub read-ahead over all streams (0: the whole pool)
     watch_reader_depth: int = 2  # ReaderHub read-ahead per stream, in buffers (2..8)
+    # https watches: the reader hub reads and opens TLS 1.3 records itself
+    # (native; openssl: SSL_read on the reader thread), on this many pool
+    # threads besides the reader thread (-1: auto, utils/cpus.py)
+    watch_tls_records: str = "native"
+    watch_tls_threads: int = -1
     hub_dispatch: bool = True  # hub-read watches feed the native pipeline with no Python call per read
     hub_framing: bool = True  # ... and the hub's thread de-chunks and splits their bodies (readerhub.inc HubFramer)
     partitioned_apply: bool = True  # a batch's apply split by pod-cache shard over the decode pool (engine.inc)
@@ -517,6 +529,9 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         watch_reader_buffers=max(2, _as_int(w.get("watch_reader_buffers", 64), "watcher.watch_reader_buffers")),
         watch_reader_max_bytes=max(0, _as_int(w.get("watch_reader_max_bytes", 0), "watcher.watch_reader_max_bytes")),
         watch_reader_depth=_reader_depth(w.get("watch_reader_depth", 2)),
+        watch_tls_records=_choice(w.get("watch_tls_records", "native"), "watcher.watch_tls_records",
+                                  ("native", "openssl")),
+        watch_tls_threads=_bounded_int(w.get("watch_tls_threads", -1), "watcher.watch_tls_threads", -1, 32),
         hub_dispatch=_as_bool(w.get("hub_dispatch", True), "watcher.hub_dispatch"),
         hub_framing=_as_bool(w.get("hub_framing", True), "watcher.hub_framing"),
         partitioned_apply=_as_bool(w.get("partitioned_apply", True), "watcher.partitioned_apply"),

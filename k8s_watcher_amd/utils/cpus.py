@@ -111,6 +111,16 @@ def auto_decode_threads(cpus: Optional[int] = None) -> int:
     return max(0, min(6, cpus - 3))
 
 
+def auto_tls_threads(cpus: Optional[int] = None) -> int:
+    """Record-opening threads of an https watch besides the reader thread
+    (watcher.watch_tls_threads: auto): AES-GCM opens ~3-5 GB/s per core and
+    the cluster watch carries 12-16 GB/s over plain TCP, so up to 3 helpers
+    where this process's share leaves room for them next to the decode
+    workers, none on a small share (the reader opens alone)."""
+    cpus = process_cpu_share() if cpus is None else cpus
+    return max(0, min(3, (cpus - 6) // 2))
+
+
 def auto_decode_spin_us(cpus: Optional[int] = None) -> float:
     """Idle spin of the decode workers before they sleep: 20 us when this
     process has CPUs to spare (a share of 8 or more), else 0. Workers still
