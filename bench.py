@@ -140,6 +140,13 @@ def parse_args(argv=None):
                     help="clusterapi.pool.io_thread: false (the event loop serves the notifier's sockets)")
     ap.add_argument("--tls", action="store_true",
                     help="https clusterapi (as production.yaml): the stub sink serves TLS with a throw-away CA")
+    ap.add_argument("--tls-records", default=None, choices=["native", "openssl"],
+                    help="watcher.watch_tls_records (https API server): the hub opens TLS 1.3 records itself, "
+                         "or SSL_read")
+    ap.add_argument("--tls-threads", type=int, default=None, help="watcher.watch_tls_threads (-1 auto)")
+    ap.add_argument("--fixture-tls", default="native", choices=["native", "python"],
+                    help="replay fixture's https: records sealed on a thread pool (native) or asyncio ssl")
+    ap.add_argument("--fixture-tls-threads", type=int, default=3, help="sealing threads per fixture worker")
     ap.add_argument("--api-tls", action="store_true",
                     help="https API server (as every real cluster): the replay fixture serves TLS, the watcher "
                          "verifies it against a throw-away CA")
@@ -328,7 +335,9 @@ class Fixtures:
         if args.tls or args.api_tls:
             from k8s_watcher_amd.testing.certs import make_pki
             self.pki = make_pki(tempfile.mkdtemp(prefix="bench-pki-"))
-        api_tls = ["--tls-cert", self.pki.server_crt, "--tls-key", self.pki.server_key] if args.api_tls else []
+        api_tls = (["--tls-cert", self.pki.server_crt, "--tls-key", self.pki.server_key,
+                    "--tls-engine", args.fixture_tls, "--tls-threads", str(args.fixture_tls_threads)]
+                   if args.api_tls else [])
         self.replay = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.cluster_replay",
                                   "--pods", str(args.pods_per_step * world),
                                   "--namespace-list", ",".join(names), "--targets", ",".join(targets),
@@ -534,6 +543,8 @@ async def rank_main(args, d: Dist) -> dict:
                         **({"watch_reader_max_bytes": args.watch_reader_max_bytes}
                            if args.watch_reader_max_bytes is not None else {}),
                         **({"watch_reader_depth": args.reader_depth} if args.reader_depth is not None else {}),
+                        **({"watch_tls_records": args.tls_records} if args.tls_records else {}),
+                        **({"watch_tls_threads": args.tls_threads} if args.tls_threads is not None else {}),
                         **({"thread_pinning": args.thread_pinning} if args.thread_pinning else {}),
                         **({"validate": args.validate} if args.validate else {}),
                         **({"hub_dispatch": args.hub_dispatch == "on"} if args.hub_dispatch else {}),
@@ -742,6 +753,18 @@ async def rank_main(args, d: Dist) -> dict:
             reader_timed = {"recv_frac": round(dr / 1e9 / elapsed, 3), "frame_frac": round(df / 1e9 / elapsed, 3),
                             "recv_gb_per_s": round(db / dr, 2) if dr else None,
                             "bytes_per_event": round(db / max(1, c["events_received"] - n0))}
+            if hub1.get("tls_taken") or hub1.get("tls_kept"):
+                # https: the reader thread's time opening records (its waits
+                # for the pool included) and each pool thread's busy share;
+                # recv_frac is then the ciphertext recv alone
+                reader_timed["tls"] = {
+                    "taken": hub1["tls_taken"], "kept": hub1["tls_kept"],
+                    "decrypt_frac": round((hub1["decrypt_ns"] - hub0["decrypt_ns"]) / 1e9 / elapsed, 3),
+                    "records": hub1["tls_records"] - hub0["tls_records"],
+                    "pooled_records": hub1["tls_pooled_records"] - hub0["tls_pooled_records"],
+                    "pool_busy_frac": [round((a[0] - b[0]) / 1e9 / elapsed, 3)
+                                       for a, b in zip(hub1["tls_pool"], hub0["tls_pool"])],
+                    "ct_gb_per_s": round((hub1["tls_ct_bytes"] - hub0["tls_ct_bytes"]) / 1e9 / elapsed, 2)}
         zc = None
         if d.rank == 0:  # the replay fixture's zero-copy sends (bytes, slot waits) so far
             reply = await fx.cmd("ZCSTATS")
@@ -1380,8 +1403,19 @@ def main(argv=None) -> int:
     lat = [x for r in d.all_gather(res["lat"]) for x in r]
     lat_hi = [x for r in d.all_gather(res["lat_hi"]) for x in r]
     sat = [x for r in d.all_gather(res["sat"]) for x in r]
+    # per rank: where its CPU went over the timed steps (process, event loop,
+    # the busiest other threads — reader, decode workers, notifier I/O — and
+    # the reader thread's recv/framing shares), so a scaling curve's per-rank
+    # loss can be put on a stage
+    reader_t = (res["reader"] or {}).get("timed") or {}
     per_rank = d.all_gather({"events": res["events"], "scopes": res["scopes"], "elapsed": round(res["elapsed"], 4),
-                             "notified": res["notified"]})
+                             "notified": res["notified"],
+                             "cpu": {"watcher": res["cpu_util"].get("watcher"),
+                                     "loop": res["cpu_util"].get("thread_loop"),
+                                     "threads": res["cpu_threads"][:8],
+                                     "reader_recv": reader_t.get("recv_frac"),
+                                     "reader_frame": reader_t.get("frame_frac")},
+                             "throttled_ms": (res["cgroup_timed"] or {}).get("throttled_ms")})
     series = _sum_series(d.all_gather(res["series"]))
     rss = d.all_gather(res["rss_mib"])
     apart = None

@@ -327,6 +327,22 @@ def _tcp_acked(sock: socket.socket) -> Optional[int]:
         return None
 
 
+RING_MAX_SLOTS = 64
+
+
+def ring_slots(step_bytes: int, bound: int) -> int:
+    """Slots for a scope whose step is ``step_bytes``: the two steps after a
+    slot's cover the peer's unread bound (3 for a step above it), else enough
+    that the steps sent between two uses of a slot exceed twice the bound;
+    0 when that takes more than RING_MAX_SLOTS (tiny scopes keep copying)."""
+    if step_bytes <= 0:
+        return 0
+    if step_bytes >= bound:
+        return 3
+    k = -(-2 * bound // step_bytes) + 2
+    return k if k <= RING_MAX_SLOTS else 0
+
+
 class ZeroCopyRing:
     """``slots`` stamped copies of one scope's step bytes in a memfd, sent with
     ``sendfile``: the kernel references the pages instead of copying them
@@ -334,12 +350,15 @@ class ZeroCopyRing:
     stream that one copy held the fixture's core).
 
     A slot's pages stay referenced by socket buffers until the watcher has
-    read them, so a slot is re-stamped for a new step only once every
-    connection that was sent from it has had its data acknowledged past that
-    point by more than the most the peer can hold unread
-    (:func:`receive_queue_bound`): ``acked - bound >= end``. Only scopes whose
-    step is larger than that bound use a ring (the cluster-wide watch: three
-    slots, so a slot is reused two whole steps later and never waits)."""
+    read them (on loopback the receiver's queue holds the sender's pages), so
+    a slot is re-stamped for a new step only once every connection that was
+    sent from it has had its data acknowledged past that point by more than
+    the most the peer can hold unread (:func:`receive_queue_bound`):
+    ``acked - bound >= end``. The cluster-wide watch's step is larger than
+    that bound: three slots, a slot is reused two whole steps later and never
+    waits. A namespace scope's step is smaller: it gets enough slots that the
+    steps sent after a slot's exceed twice the bound (:func:`ring_slots`), so
+    it does not wait either."""
 
     def __init__(self, base: np.ndarray, slots: int, bound: int) -> None:
         import mmap
@@ -401,13 +420,16 @@ class Worker:
     """One serving process: its share of the watch connections, every command."""
 
     def __init__(self, model: ClusterModel, sock: socket.socket, slice_bytes: int = 1 << 20,
-                 zero_copy: bool = True) -> None:
+                 zero_copy: bool = True, zc_budget: int = 3 << 30) -> None:
         self.m = model
         self.sock = sock
         self.slice = slice_bytes
         self.zero_copy = zero_copy
         self.rq_bound = receive_queue_bound() + (1 << 20)
         self.rings: Dict[str, ZeroCopyRing] = {}
+        self.zc_budget = zc_budget  # memfd bytes this worker may give rings (slots x step, all scopes)
+        self.zc_used = 0
+        self.no_ring: set = set()  # scopes left on the copy path (too small, or over the budget)
         self.scopes: Dict[str, ScopeStream] = {}
         self.watchers: List[Tuple[str, asyncio.StreamWriter]] = []
         self.sent: List[List[int]] = []  # [step, g0, g1) ranges of the global history sent so far
@@ -556,16 +578,19 @@ class Worker:
 
     def ring(self, name: str, w: asyncio.StreamWriter) -> Optional[ZeroCopyRing]:
         """The scope's zero-copy ring, when this connection can use one: plain
-        TCP (sendfile cannot go through TLS) and a step larger than the bound
-        a slot waits out (small namespace scopes keep copying)."""
-        if not self.zero_copy or w.get_extra_info("sslcontext") is not None:
+        TCP (sendfile cannot go through TLS), a step large enough for
+        :func:`ring_slots` and room in the worker's memfd budget."""
+        if not self.zero_copy or name in self.no_ring or w.get_extra_info("sslcontext") is not None:
             return None
         r = self.rings.get(name)
         if r is None:
             sc = self.scope(name)
-            if len(sc.base) < self.rq_bound:
+            slots = ring_slots(len(sc.base), self.rq_bound)
+            if not slots or self.zc_used + slots * len(sc.base) > self.zc_budget:
+                self.no_ring.add(name)
                 return None
-            r = self.rings[name] = ZeroCopyRing(sc.base, 3, self.rq_bound)
+            self.zc_used += slots * len(sc.base)
+            r = self.rings[name] = ZeroCopyRing(sc.base, slots, self.rq_bound)
         return r
 
     async def _send_zc(self, w: asyncio.StreamWriter, sc: ScopeStream, ring: ZeroCopyRing, k: int) -> None:
@@ -876,7 +901,8 @@ def run(args) -> None:
                             ssl_ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
                             ssl_ctx.load_cert_chain(args.tls_cert, args.tls_key)
                     asyncio.run(Worker(model, _reuseport_socket(ports[g], listen=True),
-                                       zero_copy=args.zero_copy != "off").serve(c_r, r_w, ssl_ctx))
+                                       zero_copy=args.zero_copy != "off",
+                                       zc_budget=int(args.zero_copy_budget_mb) << 20).serve(c_r, r_w, ssl_ctx))
                 finally:
                     os._exit(0)
             os.close(c_r)
@@ -947,6 +973,8 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--zero-copy", default="auto", choices=["auto", "off"],
                     help="auto: scopes whose step outgrows a peer's receive buffer are sent with sendfile "
                          "from a memfd ring (ZeroCopyRing); off: every scope is written (copied)")
+    ap.add_argument("--zero-copy-budget-mb", type=int, default=3072,
+                    help="memfd memory per worker for zero-copy rings (scopes past it copy)")
     ap.add_argument("--prototypes", type=int, default=256)
     ap.add_argument("--seed", type=int, default=0)
     run(ap.parse_args(argv))
