@@ -233,10 +233,13 @@ class WatcherService:
             # per doubling on a 256-CPU host (utils/fds.py)
             from ..utils.fds import reserve_fd_table
             reserve_fd_table(s.watcher.fd_table_reserve)
-        if s.watcher.gc_freeze:
+        if s.watcher.gc_freeze and gc.get_freeze_count() == 0:
             # what import and configuration made is permanent: the full
             # collections that starting a thousand scopes triggers then walk
-            # only the scopes' own objects (70-140 ms gen-2 pauses otherwise)
+            # only the scopes' own objects (70-140 ms gen-2 pauses otherwise).
+            # Only when nothing is frozen yet: an embedding application that
+            # froze its own objects keeps control of the permanent generation
+            # (shutdown's unfreeze would thaw its objects too)
             gc.freeze()
             self._gc_frozen = True
         if not await self.setup_k8s_client():
@@ -387,7 +390,7 @@ class WatcherService:
         if self.ns_watcher is not None:
             self._on_namespaces(self.ns_watcher.names)  # changes seen while the first scopes started
         await self._wait_synced()
-        if s.watcher.gc_freeze and not self._stop.is_set():
+        if self._gc_frozen and not self._stop.is_set():
             # the scopes' long-lived objects join the frozen set; only the young
             # generations are collected first (a full pass over a 1,000-scope
             # start's objects would hold the loop ~30 ms; cyclic garbage already

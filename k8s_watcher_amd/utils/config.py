@@ -357,7 +357,11 @@ class WatcherSettings:
     # once every scope has synced, collect and freeze what start-up left
     # (gc.freeze): later full collections then walk only objects made since,
     # not the service's long-lived ones (a 1,000-scope relist storm's gen-2
-    # pauses); unfrozen again at shutdown
+    # pauses); unfrozen again at shutdown. The cost is bounded and one-time:
+    # start-up objects that later become cyclic garbage (a namespace's
+    # reflector stopped in discover mode, the first watch connections'
+    # transport cycles) stay until shutdown, they are never re-frozen. Skipped
+    # when something is already frozen (an embedding application's own freeze)
     gc_freeze: bool = True
     # the descriptor table grown once at start to hold this many fds (a watch
     # per namespace opens two each; growing it later, with threads running,

@@ -161,3 +161,28 @@ def test_gc_freeze_after_sync_and_unfreeze_at_shutdown(freeze):
     base, during, after = run(body())
     assert base == 0 and after == 0
     assert (during > 0) == freeze
+
+
+def test_gc_freeze_leaves_an_embedders_freeze_alone():
+    """An application that froze its own objects before starting the service
+    keeps them frozen: the service neither freezes on top (its shutdown would
+    thaw everything) nor unfreezes at shutdown (round-4 advisor finding)."""
+    import gc
+
+    async def body():
+        srv, sink, svc = await start_stack(overrides={"watcher": {"gc_freeze": True}})
+        gc.freeze()
+        mine = gc.get_freeze_count()
+        try:
+            await svc.start()
+            svc.stop()
+            await svc.shutdown()
+            return mine, gc.get_freeze_count()
+        finally:
+            gc.unfreeze()
+            await sink.stop()
+            await srv.stop()
+
+    mine, after = run(body())
+    # still frozen (a few frozen objects may have been freed by refcount meanwhile)
+    assert mine > 0 and mine - 1000 < after <= mine
