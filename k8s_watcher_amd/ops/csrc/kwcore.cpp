@@ -52,6 +52,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
+#include <condition_variable>
 #include <deque>
 #include <functional>
 #include <memory>

@@ -79,7 +79,8 @@ def _native_server(pki, srv, body_parts, threads=2, key_update_at=None, forge=Fa
         if key_update_at is not None and i == key_update_at:
             conn.key_update()
         conn.send(part)
-    if forge:  # a record no key opens: 0x17 0x0303, 40 bytes of noise
+    if forge:  # a record no key opens: 0x17 0x0303, 40 bytes of noise (after the queued records)
+        conn.flush()
         os.write(conn.fileno(), b"\x17\x03\x03\x00\x28" + os.urandom(40))
         time.sleep(0.2)
     if result is not None:
