@@ -861,7 +861,9 @@ async def rank_main(args, d: Dist) -> dict:
                 "fixture_workers": shared["fixture_workers"], "sink_workers": getattr(fx, "sink_workers", None),
                 "front_ends": shared["front_ends"],
                 "cpu_util": {k: round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0
-                             if not k.startswith("thread_") or k == "thread_loop"},
+                             if not k.startswith(("thread_", "fxthread_")) or k == "thread_loop"},
+                "replay_threads": sorted((round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0
+                                          if k.startswith("fxthread_") and k in cpu1), reverse=True)[:10],
                 "cpu_threads": sorted((round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu0
                                        if k.startswith("thread_") and k != "thread_loop" and k in cpu1),
                                       reverse=True)[:8],
@@ -1262,6 +1264,17 @@ def cpu_snapshot(fx: "Fixtures", threads: bool = True) -> dict:
         out["sink"] = sum(tree(sink) for sink in fx.sinks)
     if not threads:
         return out
+    if fx.replay is not None:  # the fixture's own threads (its event loops, TLS sealing pools, writers)
+        try:
+            root = psutil.Process(fx.replay.pid)
+            for pr in [root] + root.children(recursive=True):
+                try:
+                    for th in pr.threads():
+                        out[f"fxthread_{th.id}"] = th.user_time + th.system_time
+                except psutil.NoSuchProcess:
+                    pass
+        except psutil.NoSuchProcess:
+            pass
     main = threading.get_native_id()
     for th in psutil.Process().threads():  # per thread: the event loop vs the decode workers
         out["thread_loop" if th.id == main else f"thread_{th.id}"] = th.user_time + th.system_time
@@ -1575,6 +1588,7 @@ def main(argv=None) -> int:
         "decode_pool_rank0": res["decode_pool"],
         **({"loop_probe_rank0": res["probe"]} if res["probe"] else {}),
         "cpu_other_threads_rank0": res["cpu_threads"],
+        "replay_threads_rank0": res["replay_threads"],
         # the watcher's own efficiency (the rate is bound by the replay fixture's core when it hits 1.0)
         "events_per_watcher_cpu_second": (round(res["events"] / (res["cpu_util"]["watcher"] * res["elapsed"]), 1)
                                           if res["cpu_util"].get("watcher") else None),

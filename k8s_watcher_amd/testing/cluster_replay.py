@@ -569,12 +569,19 @@ class Worker:
         every connection's send has returned."""
         try:
             n = len(sc.base)
-            # native TLS: 4 MiB per call — each call's sealing overlaps the
-            # connection's writer thread, and fewer executor round trips
-            sl = self.slice * 4 if isinstance(w, _TlsWriter) else self.slice
-            for i in range(0, n, sl):
-                view = sc.ensure(k, min(n, i + sl))
-                w.write(view[i:i + sl])
+            if isinstance(w, _TlsWriter):
+                # native TLS: the slices are queued as they are patched (the
+                # next slice's patch touches none of the earlier ones' bytes)
+                # and sealed on the TLS pool meanwhile; one drain per step,
+                # before the buffer may be patched for the next step
+                sl = self.slice * 4
+                for i in range(0, n, sl):
+                    w.write(sc.ensure(k, min(n, i + sl))[i:i + sl])
+                await w.drain()
+                return
+            for i in range(0, n, self.slice):
+                view = sc.ensure(k, min(n, i + self.slice))
+                w.write(view[i:i + self.slice])
                 await w.drain()
         except (ConnectionError, RuntimeError):
             pass
@@ -804,17 +811,29 @@ class _TlsWriter:
         if self.task is None:
             self.task = asyncio.ensure_future(self._pump())
 
+    def _send_parts(self, parts) -> None:
+        conn = self.conn
+        if conn is None:
+            raise BrokenPipeError("closed")
+        small = []
+        for p in parts:  # small pieces (a watch's backlog, event by event) are sealed together
+            if len(p) < (64 << 10):
+                small.append(p)
+                continue
+            if small:
+                conn.send(b"".join(small))
+                small = []
+            conn.send(p)
+        if small:
+            conn.send(b"".join(small))
+
     async def _pump(self) -> None:
         loop = asyncio.get_running_loop()
         try:
             while self.q:
-                parts = [self.q.popleft()]
-                size = len(parts[0])
-                while self.q and size + len(self.q[0]) <= (1 << 20):  # small pieces go out together
-                    size += len(self.q[0])
-                    parts.append(self.q.popleft())
-                data = parts[0] if len(parts) == 1 else b"".join(parts)
-                await loop.run_in_executor(self.ex, self.conn.send, data)
+                parts = list(self.q)  # everything queued so far: one executor hop
+                self.q.clear()
+                await loop.run_in_executor(self.ex, self._send_parts, parts)
         except OSError:
             self.failed = self.closed = True
             self.q.clear()
