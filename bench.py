@@ -330,7 +330,13 @@ class Fixtures:
     async def start(self, args, world: int, names, targets, rank_cpus) -> dict:
         fronts = world if args.front_ends == "per-rank" else 1
         rank_cpus = list(rank_cpus) + [None] * (world - len(rank_cpus))
-        fw = args.fixture_workers or (2 if fronts > 1 else max(2, 2 * world))
+        # replay workers per front-end: 2, or 4 when one front-end serves
+        # hundreds of namespace watches (their small steps take the copy path,
+        # which a worker pays per byte: 1,000 namespaces held two workers at
+        # ~0.9 each, profiles/r5/shards/ns1000.json)
+        cluster = args.watch_scope == "cluster" or (args.watch_scope == "auto" and world == 1)
+        many = len(names) // max(1, fronts) >= 256 and not cluster
+        fw = args.fixture_workers or (2 if fronts > 1 and not many else max(4 if many else 2, 2 * world))
         cpu_arg = ";".join(cpu_ranges(rank_cpus[g]) or "" for g in range(fronts)) if any(rank_cpus) else None
         if args.tls or args.api_tls:
             from k8s_watcher_amd.testing.certs import make_pki

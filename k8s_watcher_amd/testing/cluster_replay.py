@@ -328,8 +328,6 @@ def _tcp_acked(sock: socket.socket) -> Optional[int]:
 
 
 RING_MAX_SLOTS = 64
-
-
 def ring_slots(step_bytes: int, bound: int) -> int:
     """Slots for a scope whose step is ``step_bytes``: the two steps after a
     slot's cover the peer's unread bound (3 for a step above it), else enough
@@ -604,14 +602,24 @@ class Worker:
         return r
 
     async def _send_zc(self, w: asyncio.StreamWriter, sc: ScopeStream, ring: ZeroCopyRing, k: int) -> None:
-        """sendfile the step from its ring slot."""
+        """sendfile the step from its ring slot: straight from here while the
+        transport has nothing buffered (a small scope's step fits the socket
+        buffer: one syscall, no asyncio sendfile machinery per namespace),
+        the rest through the loop's sendfile, which waits for the socket."""
         loop = asyncio.get_running_loop()
         try:
             i = await ring.slot_for(sc, k)
             sock = w.get_extra_info("socket")
             raw = getattr(sock, "_sock", sock)  # asyncio's TransportSocket wraps the socket
             base = i * ring.n
-            await loop.sendfile(w.transport, ring.file, base, ring.n, fallback=False)
+            sent = 0
+            if w.transport.get_write_buffer_size() == 0:
+                try:
+                    sent = os.sendfile(raw.fileno(), ring.file.fileno(), base, ring.n)
+                except (BlockingIOError, InterruptedError):
+                    sent = 0
+            if sent < ring.n:
+                await loop.sendfile(w.transport, ring.file, base + sent, ring.n - sent, fallback=False)
             ring.bytes += ring.n
             ring.note_sent(i, raw)
         except (ConnectionError, RuntimeError, OSError):
