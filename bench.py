@@ -243,11 +243,31 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+_SPAWNED: set = set()  # process groups of the fixtures this process started
+
+
+def _reap_on_signal(signum, _frame) -> None:
+    """SIGTERM / SIGINT (a timeout killing the bench): the fixtures' process
+    groups go first — they run in sessions of their own and would outlive
+    us — then the default action."""
+    for pgid in list(_SPAWNED):
+        try:
+            os.killpg(pgid, signal.SIGKILL)
+        except (ProcessLookupError, PermissionError):
+            pass
+    signal.signal(signum, signal.SIG_DFL)
+    os.kill(os.getpid(), signum)
+
+
 async def spawn(*cmd: str, cpus=None):
-    return await asyncio.create_subprocess_exec(
+    # BENCH_FIXTURE_STDERR=1: the fixtures' stderr is ours (debugging a fixture)
+    p = await asyncio.create_subprocess_exec(
         *cmd, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
-        stderr=asyncio.subprocess.DEVNULL, start_new_session=True, cwd=ROOT,
+        stderr=None if os.environ.get("BENCH_FIXTURE_STDERR") else asyncio.subprocess.DEVNULL,
+        start_new_session=True, cwd=ROOT,
         preexec_fn=(lambda: os.sched_setaffinity(0, cpus)) if cpus else None)
+    _SPAWNED.add(p.pid)
+    return p
 
 
 def fixture_cpus(all_cpus: set, watcher_domains: list) -> "set | None":
@@ -443,6 +463,7 @@ class Fixtures:
             # the whole group, not just its leader, so nothing of the bench
             # outlives it (the driver counted 2)
             await reap_group(p.pid)
+            _SPAWNED.discard(p.pid)
             transport = getattr(p, "_transport", None)
             if transport is not None:
                 transport.close()  # close pipes while the loop is alive (no __del__ noise)
@@ -1411,6 +1432,8 @@ def main(argv=None) -> int:
     # watcher start threads before the service does (utils/fds.py)
     from k8s_watcher_amd.utils.fds import reserve_fd_table
     reserve_fd_table(16384)
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, _reap_on_signal)
     d = Dist()
     res = asyncio.run(rank_main(args, d))
     if res.get("soak"):

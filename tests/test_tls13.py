@@ -196,3 +196,60 @@ def test_hkdf_traffic_keys_match_rfc8448():
     server_application_traffic_secret_0 gives the published write key and iv
     (the records above also open against OpenSSL's own sealing)."""
     assert load().tls13_selftest()
+
+
+def test_many_connections_share_the_sealing_pool(pki):
+    """Several connections of one TlsServerContext send at once from their own
+    threads (the fixture's executor): its CryptoPool runs one batch at a time
+    and every stream arrives byte-exact (a shared-lock race here once aborted
+    the fixture with 64 namespace watches)."""
+    mod = load()
+    tls = mod.TlsServerContext(pki.server_crt, pki.server_key, threads=3)
+    srv = _listener()
+    n = 6
+    bodies = [os.urandom(1_500_000) for _ in range(n)]
+
+    def serve_one():
+        c, _ = srv.accept()
+        conn = tls.accept(c.detach())
+        req = b""
+        while not req.endswith(b"\r\n\r\n"):
+            d = conn.recv(65536)
+            if d is None:
+                time.sleep(0.001)
+                continue
+            req += d
+        i = int(req.split(b"/")[1].split(b" ")[0])
+        for off in range(0, len(bodies[i]), 300_000):
+            conn.send(bodies[i][off:off + 300_000])
+        conn.close()
+
+    threads = [threading.Thread(target=serve_one) for _ in range(n)]
+    for t in threads:
+        t.start()
+    hub = mod.ReaderHub(1 << 20, 32)
+    hub.set_tls(True, 2)
+    ctx = mod.TlsContext(ca_pem=open(pki.ca_crt, "rb").read())
+    sids = {}
+    for i in range(n):
+        c = socket.create_connection(srv.getsockname())
+        sids[hub.add_tls(c.detach(), ctx, "127.0.0.1", b"GET /%d HTTP/1.1\r\nHost: x\r\n\r\n" % i)] = i
+    got = {sid: bytearray() for sid in sids}
+    ends = {}
+    t_end = time.monotonic() + 60
+    while len(ends) < n and time.monotonic() < t_end:
+        for s, buf, view, _ns, err in hub.take():
+            if view is None:
+                ends[s] = err
+            else:
+                got[s] += view
+                view.release()
+                hub.release(buf)
+        time.sleep(0.001)
+    for t in threads:
+        t.join()
+    assert all(e == 0 for e in ends.values()) and len(ends) == n
+    for sid, i in sids.items():
+        assert bytes(got[sid]) == bodies[i]
+    hub.close()
+    srv.close()
