@@ -130,8 +130,9 @@ def parse_args(argv=None):
                     help="watcher.hub_dispatch: hub-read watches feed the native pipeline directly")
     ap.add_argument("--partitioned-apply", default=None, choices=["on", "off"],
                     help="watcher.partitioned_apply: a batch's apply split by pod-cache shard over the decode pool")
-    ap.add_argument("--hub-framing", default=None, choices=["on", "off"],
-                    help="watcher.hub_framing: the reader hub's thread de-chunks and splits bound watch bodies")
+    ap.add_argument("--hub-framing", default=None, choices=["auto", "on", "off"],
+                    help="watcher.hub_framing: the reader hub's thread de-chunks and splits bound watch bodies "
+                         "(auto: with several watch scopes)")
     ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
     ap.add_argument("--io-thread", action="store_true",
                     help="serve the C++ notifier core's sockets on its own thread (clusterapi.pool.io_thread)")
@@ -575,7 +576,7 @@ async def rank_main(args, d: Dist) -> dict:
                         **({"thread_pinning": args.thread_pinning} if args.thread_pinning else {}),
                         **({"validate": args.validate} if args.validate else {}),
                         **({"hub_dispatch": args.hub_dispatch == "on"} if args.hub_dispatch else {}),
-                        **({"hub_framing": args.hub_framing == "on"} if args.hub_framing else {}),
+                        **({"hub_framing": args.hub_framing} if args.hub_framing else {}),
                         **({"partitioned_apply": args.partitioned_apply == "on"} if args.partitioned_apply else {}),
                         **({"state_format": args.state_format} if args.state_format else {}),
                         # placement already pinned this thread (the decode workers inherit it)

@@ -323,7 +323,8 @@ class WatcherService:
                 self._reader_hub = WatchReaderHub(s.watcher.watch_read_bytes or (4 << 20),
                                                   s.watcher.watch_reader_buffers,
                                                   max_bytes=s.watcher.watch_reader_max_bytes,
-                                                  frame=s.watcher.hub_framing,
+                                                  frame=(s.watcher.hub_framing == "on" or
+                                                         (s.watcher.hub_framing == "auto" and self._multi)),
                                                   depth=s.watcher.watch_reader_depth,
                                                   tls_records=s.watcher.watch_tls_records == "native",
                                                   tls_threads=(s.watcher.watch_tls_threads

@@ -42,8 +42,9 @@ class WatchReaderHub:
         self.loop = loop or asyncio.get_running_loop()
         # max_bytes: read-ahead over all streams (0: the whole pool); frame: the
         # hub's thread de-chunks and splits bound bodies (watcher.hub_framing)
+        self.frame = bool(frame)
         self.core = native.load().ReaderHub(max(64 * 1024, int(buf_bytes)), max(2, int(nbufs)),
-                                            max(0, int(max_bytes)), frame=bool(frame))
+                                            max(0, int(max_bytes)), frame=self.frame)
         # depth: buffers read ahead per stream (watcher.watch_reader_depth)
         if depth != 2:
             self.core.set_depth(int(depth))

@@ -174,6 +174,12 @@ def _as_int(value: Any, key: str) -> int:
     return out
 
 
+def _hub_framing(value: Any) -> str:
+    if value == "auto":
+        return "auto"
+    return "on" if _as_bool(value, "watcher.hub_framing") else "off"
+
+
 def _bounded_int(value: Any, key: str, lo: int, hi: int) -> int:
     n = _as_int(value, key)
     if not lo <= n <= hi:
@@ -328,7 +334,12 @@ class WatcherSettings:
     watch_tls_records: str = "native"
     watch_tls_threads: int = -1
     hub_dispatch: bool = True  # hub-read watches feed the native pipeline with no Python call per read
-    hub_framing: bool = True  # ... and the hub's thread de-chunks and splits their bodies (readerhub.inc HubFramer)
+    # ... and the hub's thread de-chunks and splits their bodies (readerhub.inc
+    # HubFramer): auto = with several watch scopes (namespace watches: the
+    # reader has time, the loop has per-stream work), not for the one
+    # cluster-wide watch, whose reader thread is the bound (it then only
+    # receives; the loop frames: profiles/r5/framing_ab, r5/framing_many)
+    hub_framing: str = "auto"  # auto | on | off
     partitioned_apply: bool = True  # a batch's apply split by pod-cache shard over the decode pool (engine.inc)
     thread_pinning: str = "auto"  # auto: loop thread and reader thread on cores of their own in one L3 | loop | none
     retry: RetryPolicy = field(default_factory=lambda: RetryPolicy(3, 5.0))
@@ -537,7 +548,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
                                   ("native", "openssl")),
         watch_tls_threads=_bounded_int(w.get("watch_tls_threads", -1), "watcher.watch_tls_threads", -1, 32),
         hub_dispatch=_as_bool(w.get("hub_dispatch", True), "watcher.hub_dispatch"),
-        hub_framing=_as_bool(w.get("hub_framing", True), "watcher.hub_framing"),
+        hub_framing=_hub_framing(w.get("hub_framing", "auto")),
         partitioned_apply=_as_bool(w.get("partitioned_apply", True), "watcher.partitioned_apply"),
         malloc_trim_seconds=_bounded_float(w.get("malloc_trim_seconds", 60.0), "watcher.malloc_trim_seconds",
                                            0.0, 86400.0),

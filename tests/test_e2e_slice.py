@@ -186,3 +186,22 @@ def test_gc_freeze_leaves_an_embedders_freeze_alone():
     mine, after = run(body())
     # still frozen (a few frozen objects may have been freed by refcount meanwhile)
     assert mine > 0 and mine - 1000 < after <= mine
+
+
+@pytest.mark.parametrize("scope,framing,want", [("client", "auto", False), ("discover", "auto", True),
+                                                ("client", "on", True), ("discover", "off", False)])
+def test_hub_framing_auto_follows_the_watch_shape(scope, framing, want):
+    """watcher.hub_framing: auto — the reader thread frames bodies when there
+    are several watch scopes, and leaves the one cluster-wide watch's framing
+    to the loop (that reader thread is the bound: profiles/r5/framing_ab)."""
+    async def body():
+        srv, sink, svc = await start_stack(overrides={"watcher": {"namespace_scope": scope, "hub_framing": framing}})
+        await svc.start()
+        got = svc._reader_hub.frame
+        svc.stop()
+        await svc.shutdown()
+        await sink.stop()
+        await srv.stop()
+        return got
+
+    assert run(body()) is want
