@@ -1033,6 +1033,10 @@ class PhaseSampler:
         self._fx_pids = self._fixture_pids()
         self._clk = time.pthread_getcpuclockid(threading.get_ident())  # the loop thread's CPU clock
         self._hz = os.sysconf("SC_CLK_TCK")
+        # the loop thread's scheduler accounting: time it was runnable but not
+        # running (preempted by another thread or tenant) — what tells a
+        # blocked loop from a busy one when a tick waits
+        self._loop_schedstat = f"/proc/self/task/{threading.get_native_id()}/schedstat"
 
     def _fixture_pids(self) -> dict:
         import psutil
@@ -1061,6 +1065,18 @@ class PhaseSampler:
                 pass
         return tot / self._hz
 
+    @staticmethod
+    def _runq_ns(paths) -> int:
+        """Summed run-queue wait (schedstat's second field, ns) of tasks."""
+        tot = 0
+        for path in paths:
+            try:
+                with open(path, "rb") as fh:
+                    tot += int(fh.read().split()[1])
+            except (OSError, IndexError, ValueError):
+                pass
+        return tot
+
     def _gc_cb(self, phase: str, info: dict) -> None:
         if phase == "start":
             self._gc_t0 = time.perf_counter()
@@ -1074,7 +1090,8 @@ class PhaseSampler:
         c = self.c
         out = {"events": c["events_received"], "trims": c.get("malloc_trims", 0),
                "trim_us": c.get("malloc_trim_us", 0), "io_switches": c.get("notify_io_switches", 0),
-               "loop_cpu": time.clock_gettime(self._clk), "gc_ms": self._gc_ms}
+               "loop_cpu": time.clock_gettime(self._clk), "gc_ms": self._gc_ms,
+               "loop_runq_ns": self._runq_ns((self._loop_schedstat,))}
         if self.hub is not None:
             st = self.hub.stats()
             out["starved"] = st.get("starved", 0)
@@ -1083,6 +1100,7 @@ class PhaseSampler:
         if self.fx.replay is not None:
             out["replay_cpu"] = self._proc_cpu(self._fx_pids["replay"])
             out["sink_cpu"] = self._proc_cpu(self._fx_pids["sink"])
+            out["sink_runq_ns"] = self._runq_ns(f"/proc/{pid}/schedstat" for pid in self._fx_pids["sink"])
         return out
 
     def start(self) -> "PhaseSampler":
@@ -1117,6 +1135,7 @@ class PhaseSampler:
                "loop_lag_max_ms": round(lag["max_us"] / 1e3, 3), "loop_lag_mean_us": round(lag["mean_us"], 1),
                "loop_lag_over_250us": lag["over_250us"], "loop_lag_over_1ms": lag["over_1ms"],
                "loop_cpu": round(b["loop_cpu"] - a["loop_cpu"], 3),
+               "loop_runq_ms": round((b["loop_runq_ns"] - a["loop_runq_ns"]) / 1e6, 3),
                "gc_ms": round(b["gc_ms"] - a["gc_ms"], 2), "gc_max_ms": round(self._gc_max, 2),
                "trims": b["trims"] - a["trims"], "trim_ms": round((b["trim_us"] - a["trim_us"]) / 1e3, 2),
                "io_switches": b["io_switches"] - a["io_switches"]}
@@ -1132,6 +1151,7 @@ class PhaseSampler:
         if "replay_cpu" in b:
             row["replay_cpu"] = round(b["replay_cpu"] - a["replay_cpu"], 2)
             row["sink_cpu"] = round(b["sink_cpu"] - a["sink_cpu"], 2)
+            row["sink_runq_ms"] = round((b["sink_runq_ns"] - a["sink_runq_ns"]) / 1e6, 3)
         row["sampler_ms"] = round((time.perf_counter() - t_a) * 1e3, 3)
         self.rows.append(row)
         self._base = b
@@ -1153,6 +1173,9 @@ class PhaseSampler:
         return self.rows
 
     SEGMENTS = ("reader_to_loop", "notifier_queue", "sink_rtt")
+    # a segment's time explained by the scheduler: the loop thread (or the
+    # sink's processes) runnable but not running for >= 1 ms that second
+    CAUSES = SEGMENTS + ("loop_preempted", "sink_preempted")
 
     def _attribute(self, raw: bytes) -> None:
         """Latency per second by ack time, and each > 1 ms sample's time split
@@ -1180,7 +1203,12 @@ class PhaseSampler:
                 s = seg[m][slow]
                 tot = s.sum(axis=0)
                 row["outlier_ms"] = {name: round(int(s[:, j].max()) / 1e6, 3) for j, name in enumerate(self.SEGMENTS)}
-                row["cause"] = self.SEGMENTS[int(tot.argmax())]
+                cause = self.SEGMENTS[int(tot.argmax())]
+                if cause == "reader_to_loop" and row.get("loop_runq_ms", 0) >= 1.0:
+                    cause = "loop_preempted"
+                elif cause == "sink_rtt" and row.get("sink_runq_ms", 0) >= 1.0:
+                    cause = "sink_preempted"
+                row["cause"] = cause
 
 
 def explain_seconds(rows: list, key: str = "events", low: float = 0.9) -> dict:
@@ -1694,10 +1722,11 @@ def lag_summary(rows: list) -> "dict | None":
     return {"seconds": len(rows), "median_max_ms": mx[len(mx) // 2], "max_ms": mx[-1],
             "seconds_max_over_1ms": sum(1 for x in mx if x > 1.0),
             "seconds_lat_over_1ms": len(slow),
-            "causes": {c: sum(1 for r in slow if r.get("cause") == c) for c in PhaseSampler.SEGMENTS
+            "causes": {c: sum(1 for r in slow if r.get("cause") == c) for c in PhaseSampler.CAUSES
                        if any(r.get("cause") == c for r in slow)},
             "outliers": [{k: r.get(k) for k in ("t", "lat_over_1ms", "lat_max_ms", "cause", "loop_lag_max_ms",
-                                                "gc_max_ms", "trims", "io_switches")} for r in slow[:8]]}
+                                                "loop_runq_ms", "loop_cpu", "sink_runq_ms", "gc_max_ms", "trims",
+                                                "io_switches")} for r in slow[:8]]}
 
 
 if __name__ == "__main__":

@@ -82,7 +82,7 @@ def check_headline(proc, out, left):
     # every second of the 1k ev/s phase with a > 1 ms notification names its cause
     rows = d["latency_high_seconds_rank0"]["rows"]
     assert rows and all("loop_lag_max_ms" in r and "sampler_ms" in r and "lat_n" in r for r in rows)
-    assert all(r.get("cause") in bench.PhaseSampler.SEGMENTS for r in rows if r.get("lat_over_1ms"))
+    assert all(r.get("cause") in bench.PhaseSampler.CAUSES for r in rows if r.get("lat_over_1ms"))
     assert sum(r["lat_n"] for r in rows) == head["latency_1k"]["samples"]
     # stderr: the one line naming the full record
     assert len(proc.stderr.strip().splitlines()) <= 2, proc.stderr[-2000:]
@@ -121,6 +121,11 @@ def test_attribution_names_the_segment_that_took_the_time():
     assert r2["lat_n"] == 1 and r2["cause"] == "reader_to_loop"
     summary = bench.lag_summary([dict(r, loop_lag_max_ms=0.1) for r in s.rows])
     assert summary["seconds_lat_over_1ms"] == 2 and summary["causes"] == {"sink_rtt": 1, "reader_to_loop": 1}
+    # the same seconds when the scheduler kept the loop thread (or the sink)
+    # runnable but off a CPU for >= 1 ms: the cause is the preemption
+    s.rows = [{"t": 1.0}, {"t": 2.0, "sink_runq_ms": 1.7}, {"t": 3.0, "loop_runq_ms": 2.4}]
+    s._attribute(np.array(samples, dtype=np.int64).tobytes())
+    assert [r.get("cause") for r in s.rows] == [None, "sink_preempted", "loop_preempted"]
 
 
 def test_loop_lag_probe_sees_a_blocked_loop():
