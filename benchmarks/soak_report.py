@@ -4,9 +4,10 @@
     python -m benchmarks.soak_report profiles/r5/soak_final.json [--title "..."]
 
 Correctness (steps, failures, duplicates), the last process's memory (RSS
-and the C heap's in-use bytes, least-squares slopes from +0.5 h, +1 h and
-+2 h of its life), and the apply-path counters it sampled (which native
-paths ran, and that they ran throughout).
+and the C heap's in-use bytes, least-squares slopes from +0.5 h, +1 h, +2 h
+and +4 h of its life, and the free bytes the allocator keeps — RSS that is
+not live data), and the apply-path counters it sampled (which native paths
+ran, and that they ran throughout).
 """
 
 from __future__ import annotations
@@ -53,8 +54,8 @@ def main(argv=None) -> None:
     out.append(f"**Last process** (pid {last_pid}, {(mine[-1]['t'] - t0) / 3600:.2f} h, {len(mine)} samples):")
     out.append("")
     out.append("| window | RSS first → last (MiB) | RSS slope (MiB/h) | C heap in use first → last (MiB) | "
-               "C heap slope (MiB/h) |")
-    out.append("|---|---|---|---|---|")
+               "C heap slope (MiB/h) | C heap free, kept by the allocator, first → last (MiB) |")
+    out.append("|---|---|---|---|---|---|")
     for hours in (0.5, 1.0, 2.0, 4.0):
         w = [x for x in mine if x["t"] - t0 >= hours * 3600]
         if len(w) < 3:
@@ -62,9 +63,10 @@ def main(argv=None) -> None:
         xs = [(x["t"] - t0) / 3600 for x in w]
         rss = [x["rss_mb"] for x in w]
         heap = [x.get("malloc_in_use_bytes", 0) / 2 ** 20 for x in w]
+        free = [x.get("malloc_free_bytes", 0) / 2 ** 20 for x in w]
         rs, hs = slope(xs, rss), slope(xs, heap)
         out.append(f"| from +{hours:g} h | {rss[0]:.1f} → {rss[-1]:.1f} | {rs:+.2f} | {heap[0]:.1f} → {heap[-1]:.1f} "
-                   f"| {hs:+.2f} |")
+                   f"| {hs:+.2f} | {free[0]:.1f} → {free[-1]:.1f} |")
     keys = ("apply_partitioned_batches", "apply_partitioned_lines", "apply_tail_submits", "apply_tail_lock_runs",
             "apply_serial_lines", "apply_tail_serial_lines")
     if all(k in mine[-1] for k in keys):
