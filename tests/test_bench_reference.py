@@ -38,7 +38,7 @@ def test_reference_rate_independent_of_history_length():
         for rounds in (1, 24):
             runs[rounds].append(_bench(rounds))
         b = best()
-        if pair >= 1 and abs(b[24] - b[1]) <= 0.15 * b[1]:
+        if pair >= 1 and b[24] >= 0.85 * b[1]:
             break
     for ref in runs[1] + runs[24]:
         assert ref["events"] == 1500
@@ -49,5 +49,5 @@ def test_reference_rate_independent_of_history_length():
         # not O(history) (round 3: seconds at 24 rounds)
         assert ref["first_event_after_s"] < 0.5, ref
     b = best()
-    # 24x the history, the same rate
-    assert abs(b[24] - b[1]) <= 0.15 * b[1], (b, runs)
+    # 24x the history, no slower (a faster best at 24 rounds is the shared CPU's noise)
+    assert b[24] >= 0.85 * b[1], (b, runs)
