@@ -48,7 +48,10 @@ def test_https_api_server_bench_line_is_valid():
                           "--pods-per-step", "1000", "--ref-events", "0", "--latency-seconds", "1",
                           "--latency-rate-high", "0", "--api-tls"])
     assert line["config"]["api_server"] == "https" and line["verify"]["exactly_once"]
-    assert line["watch_reader_rank0"]["mode"] == "native"
+    reader = line["watch_reader_rank0"]
+    assert reader["mode"] == "native"
+    # the hub's own TLS 1.3 record layer carried it, not an SSL_read fallback
+    assert reader["tls_taken"] >= 1 and reader["tls_kept"] == 0 and reader["tls_records"] > 0
 
 
 def test_reader_hub_on_host():

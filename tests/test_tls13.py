@@ -253,3 +253,369 @@ def test_many_connections_share_the_sealing_pool(pki):
         assert bytes(got[sid]) == bodies[i]
     hub.close()
     srv.close()
+
+
+# ----------------------------------------------------------------------------
+# round 6: the record layer's less travelled branches (VERDICT r5 "what's
+# weak" #2) — padding, split post-handshake messages, alerts, every suite,
+# a malformed header behind good records, truncation, ring memory
+
+
+def _serve(pki, srv, script, suites=None, result=None, threads=2):
+    """One connection on the native fixture server: read the request, then
+    ``script(conn)`` does the sending; close_notify after it unless it
+    returns False."""
+    tls = load().TlsServerContext(pki.server_crt, pki.server_key, threads=threads, ciphersuites=suites)
+    c, _ = srv.accept()
+    conn = tls.accept(c.detach())
+    req = b""
+    t_end = time.monotonic() + 10
+    while not req.endswith(b"\r\n\r\n") and time.monotonic() < t_end:
+        d = conn.recv(65536)
+        if d is None:
+            time.sleep(0.001)
+            continue
+        if not d:
+            break
+        req += d
+    if result is not None:
+        result["cipher"] = conn.cipher()
+    if script(conn) is not False:
+        conn.close()
+    else:
+        conn.flush()
+
+
+def _run(pki, script, suites=None, buf=1 << 20, nbufs=8, threads=2, result=None):
+    srv = _listener()
+    res = {} if result is None else result
+    t = threading.Thread(target=_serve, args=(pki, srv, script), kwargs={"suites": suites, "result": res})
+    t.start()
+    hub = load().ReaderHub(buf, nbufs)
+    hub.set_tls(True, threads)
+    sid = _client(hub, pki, srv.getsockname()[1])
+    got, end = _drain(hub, sid)
+    t.join()
+    st = hub.stats()
+    err = hub.error_text(sid)
+    hub.close()
+    srv.close()
+    return got, end, st, err, res
+
+
+@pytest.mark.parametrize("pad", [1, 300, 4096])
+def test_padded_records_are_byte_exact(pki, pad):
+    """RFC 8446 §5.4: zero padding after the content type, inside the
+    encryption — the hub finds the type as the last non-zero byte."""
+    big, small = os.urandom(2_000_000), os.urandom(777)
+
+    def script(conn):
+        conn.send(big, pad=pad)
+        conn.send(small, pad=pad)
+
+    got, end, st, _err, _ = _run(pki, script)
+    assert end == 0 and got == big + small
+    assert st["tls_taken"] == 1
+    assert st["tls_records"] >= len(big) // (16384 - pad)
+
+
+def _ticket(n):
+    """A NewSessionTicket handshake message (RFC 8446 §4.6.1) with an n-byte ticket."""
+    body = (7200).to_bytes(4, "big") + os.urandom(4) + b"\x08" + os.urandom(8) + n.to_bytes(2, "big") + os.urandom(n) \
+        + b"\x00\x00"
+    return b"\x04" + len(body).to_bytes(3, "big") + body
+
+
+def test_post_handshake_messages_split_over_records(pki):
+    """A NewSessionTicket cut over two records, then a KeyUpdate cut after
+    its second byte: both are reassembled (§5.1), the ticket is skipped, and
+    every record after the KeyUpdate opens with the next key."""
+    a, b, c = os.urandom(300_000), os.urandom(5_000), os.urandom(900_000)
+
+    def script(conn):
+        conn.send(a)
+        t = _ticket(3000)
+        conn.send_record(22, t, split=1500)
+        conn.send(b)
+        conn.key_update(split=2)
+        conn.send(c)
+
+    got, end, st, err, _ = _run(pki, script)
+    assert end == 0 and got == a + b + c, err
+    assert st["tls_tickets"] == 1 and st["tls_key_updates"] == 1
+
+
+def test_key_update_split_at_every_offset(pki):
+    parts = [os.urandom(50_000) for _ in range(5)]
+
+    def script(conn):
+        for i, p in enumerate(parts):
+            conn.send(p)
+            if i < 4:
+                conn.key_update(split=i + 1)  # cut after byte 1, 2, 3, 4 of the 5-byte message
+
+    got, end, st, err, _ = _run(pki, script, threads=0)
+    assert end == 0 and got == b"".join(parts), err
+    assert st["tls_key_updates"] == 4
+
+
+def test_record_interleaved_with_a_split_message_fails(pki):
+    def script(conn):
+        conn.send(b"a" * 1000)
+        t = _ticket(100)
+        conn.send_record(22, t[:50])  # half a message ...
+        conn.send(b"b" * 10)          # ... then application data: not allowed (§5.1)
+
+    got, end, _st, err, _ = _run(pki, script)
+    assert end is not None and end < 0
+    assert got == b"a" * 1000
+    assert "interleaved" in err
+
+
+def test_data_after_a_key_update_in_its_record_fails(pki):
+    def script(conn):
+        conn.send(b"x" * 100)
+        conn.send_record(22, bytes([24, 0, 0, 1, 0]) + _ticket(10))  # KeyUpdate must end its record
+        return False
+
+    got, end, _st, err, _ = _run(pki, script)
+    assert end is not None and end < 0 and got == b"x" * 100
+    assert "key update" in err
+
+
+@pytest.mark.parametrize("desc", [40, 80])
+def test_fatal_alert_ends_the_stream_with_an_error(pki, desc):
+    """A fatal alert (handshake_failure, internal_error) is an error with its
+    code — unlike close_notify — and what came before it is delivered."""
+    body = os.urandom(200_000)
+
+    def script(conn):
+        conn.send(body)
+        conn.send_record(21, bytes([2, desc]))
+        return False
+
+    got, end, _st, err, _ = _run(pki, script)
+    assert end is not None and end < 0
+    assert got == body
+    assert f"alert {desc}" in err
+
+
+@pytest.mark.parametrize("suite,key_bits", [("TLS_AES_128_GCM_SHA256", 128), ("TLS_AES_256_GCM_SHA384", 256)])
+def test_each_aes_gcm_suite_is_taken_over(pki, suite, key_bits):
+    """Both AES-GCM suites, forced on the server (an OpenSSL client offers
+    AES-256 first, so AES-128 needs the server to insist): HKDF over
+    SHA-256 / SHA-384, 16- / 32-byte keys, across a KeyUpdate."""
+    a, b = os.urandom(1_500_000), os.urandom(600_000)
+
+    def script(conn):
+        conn.send(a)
+        conn.key_update()
+        conn.send(b)
+
+    got, end, st, err, res = _run(pki, script, suites=suite)
+    assert res["cipher"] == (suite, True)
+    assert end == 0 and got == a + b, err
+    assert st["tls_taken"] == 1 and st["tls_kept"] == 0 and st["tls_key_updates"] == 1
+
+
+def test_chacha20_peer_stays_on_ssl_read(pki):
+    """A server that only speaks ChaCha20-Poly1305: the hub cannot open its
+    records, so the stream stays on SSL_read (tls_kept) — and a KeyUpdate
+    there is OpenSSL's business — with the same bytes delivered."""
+    a, b = os.urandom(800_000), os.urandom(300_000)
+
+    def script(conn):
+        conn.send(a)
+        conn.key_update()
+        conn.send(b)
+
+    got, end, st, err, res = _run(pki, script, suites="TLS_CHACHA20_POLY1305_SHA256")
+    assert res["cipher"] == ("TLS_CHACHA20_POLY1305_SHA256", False)
+    assert end == 0 and got == a + b, err
+    assert st["tls_taken"] == 0 and st["tls_kept"] == 1
+
+
+def _paused_run(pki, send):
+    """The hub's stream is paused once the request is in, the server writes
+    everything ``send(conn)`` makes, then the stream resumes: the hub meets
+    it all in one receive."""
+    srv = _listener()
+    sent = threading.Event()
+
+    def script(conn):
+        ready.wait(10)
+        send(conn)
+        sent.set()
+        time.sleep(0.3)
+        return False
+
+    ready = threading.Event()
+    t = threading.Thread(target=_serve, args=(pki, srv, script))
+    t.start()
+    hub = load().ReaderHub(1 << 20, 8)
+    hub.set_tls(True, 2)
+    sid = _client(hub, pki, srv.getsockname()[1])
+    t_end = time.monotonic() + 10
+    while hub.stats()["tls_taken"] + hub.stats()["tls_kept"] == 0 and time.monotonic() < t_end:
+        time.sleep(0.002)  # the handshake and the request are done
+    hub.pause(sid, True)
+    ready.set()
+    sent.wait(10)
+    time.sleep(0.1)
+    hub.pause(sid, False)
+    got, end = _drain(hub, sid)
+    t.join()
+    err = hub.error_text(sid)
+    st = hub.stats()
+    hub.close()
+    srv.close()
+    return got, end, err, st
+
+
+def test_bad_header_after_good_records_in_one_read_delivers_them_all(pki):
+    """Several good records and then a malformed header arrive in one
+    receive: every good record is delivered, then the stream fails
+    (round-5 advisor: the failure used to cut the batch after its first)."""
+    parts = [bytes([65 + i]) * 3000 for i in range(4)]
+
+    def send(conn):
+        for p in parts:
+            conn.send(p)
+        conn.flush()
+        os.write(conn.fileno(), b"\x16\x03\x03\x00\x20" + b"\x00" * 32)  # a plaintext handshake header
+
+    got, end, err, st = _paused_run(pki, send)
+    assert got == b"".join(parts)
+    assert end is not None and end < 0 and "unexpected record" in err
+    assert st["tls_records"] == 4
+
+
+def test_truncated_inside_a_record_is_an_error(pki):
+    """The peer closes TCP in the middle of a record without close_notify:
+    a truncated stream, reported as an error (as OpenSSL's own read would),
+    not as an orderly close."""
+    body = os.urandom(40_000)
+
+    def send(conn):
+        conn.send(body)
+        conn.flush()
+        fd = conn.fileno()
+        os.write(fd, b"\x17\x03\x03\x04\x00" + os.urandom(100))  # header of 1,024 bytes, 100 of them
+        s = socket.socket(fileno=os.dup(fd))
+        s.shutdown(socket.SHUT_WR)
+        s.close()
+
+    got, end, err, _st = _paused_run(pki, send)
+    assert got == body
+    assert end is not None and end < 0 and "truncated" in err
+
+
+def test_ring_memory_is_counted_in_the_pool_and_shrinks_with_the_class(pki):
+    """The ciphertext ring is hub memory: it shows in ``allocated_bytes``
+    (``watch_reader_allocated_bytes``) and ``tls_ring_bytes``, grows with the
+    stream's buffer class and shrinks back when a quiet stream's class
+    drops (round-5 advisor)."""
+    burst = os.urandom(12_000_000)
+    seen = {"max_ring": 0, "max_alloc": 0}
+    srv = _listener()
+    go_quiet = threading.Event()
+
+    def script(conn):
+        conn.send(burst)
+        conn.flush()
+        go_quiet.wait(20)
+        for _ in range(12):
+            conn.send(b"q" * 500)
+            conn.flush()
+            time.sleep(0.03)
+
+    t = threading.Thread(target=_serve, args=(pki, srv, script))
+    t.start()
+    hub = load().ReaderHub(1 << 20, 8)
+    hub.set_tls(True, 2)
+    sid = _client(hub, pki, srv.getsockname()[1])
+    got, end = bytearray(), None
+    t_end = time.monotonic() + 30
+    while end is None and time.monotonic() < t_end:
+        st = hub.stats()
+        seen["max_ring"] = max(seen["max_ring"], st["tls_ring_bytes"])
+        seen["max_alloc"] = max(seen["max_alloc"], st["allocated_bytes"])
+        assert st["allocated_bytes"] >= st["tls_ring_bytes"]
+        for _s, buf, view, _ns, err in hub.take():
+            if view is None:
+                end = err
+                continue
+            got += view
+            view.release()
+            hub.release(buf)
+            if len(got) >= len(burst):
+                go_quiet.set()
+        if len(got) >= len(burst) + 8 * 500 and end is None:  # quiet for a while, stream still open
+            seen["quiet_ring"] = hub.stats()["tls_ring_bytes"]
+        time.sleep(0.004)  # a slow consumer: the stream's buffers fill and its class grows
+    t.join()
+    assert end == 0 and bytes(got) == burst + b"q" * 6000
+    assert seen["max_ring"] > 1 << 20            # two 1 MiB batches' worth while busy
+    assert 0 < seen["quiet_ring"] < 200 << 10    # back to the small class's ring once quiet
+    assert seen["max_alloc"] <= (8 << 20) + (3 << 20)
+    assert hub.stats()["tls_ring_bytes"] == 0    # released with the stream
+    hub.close()
+    srv.close()
+
+
+def test_many_tls_streams_share_the_pool_with_their_rings(pki):
+    """Sixteen https streams on a 1 MiB pool: rings and buffers together
+    stay near the pool's memory, and every stream is delivered whole (a
+    stream's first buffer never waits behind rings)."""
+    mod = load()
+    tls = mod.TlsServerContext(pki.server_crt, pki.server_key, threads=2)
+    srv = _listener()
+    n = 16
+    bodies = [os.urandom(400_000) for _ in range(n)]
+
+    def serve_one():
+        c, _ = srv.accept()
+        conn = tls.accept(c.detach())
+        req = b""
+        while not req.endswith(b"\r\n\r\n"):
+            d = conn.recv(65536)
+            if d is None:
+                time.sleep(0.001)
+                continue
+            req += d
+        i = int(req.split(b"/")[1].split(b" ")[0])
+        conn.send(bodies[i])
+        conn.close()
+
+    threads = [threading.Thread(target=serve_one) for _ in range(n)]
+    for t in threads:
+        t.start()
+    hub = mod.ReaderHub(256 << 10, 4)
+    hub.set_tls(True, 2)
+    ctx = mod.TlsContext(ca_pem=open(pki.ca_crt, "rb").read())
+    sids = {}
+    for i in range(n):
+        c = socket.create_connection(srv.getsockname())
+        sids[hub.add_tls(c.detach(), ctx, "127.0.0.1", b"GET /%d HTTP/1.1\r\nHost: x\r\n\r\n" % i)] = i
+    got = {sid: bytearray() for sid in sids}
+    ends, peak = {}, 0
+    t_end = time.monotonic() + 60
+    while len(ends) < n and time.monotonic() < t_end:
+        peak = max(peak, hub.stats()["allocated_bytes"])
+        for s, buf, view, _ns, err in hub.take():
+            if view is None:
+                ends[s] = err
+            else:
+                got[s] += view
+                view.release()
+                hub.release(buf)
+        time.sleep(0.001)
+    for t in threads:
+        t.join()
+    assert len(ends) == n and all(e == 0 for e in ends.values())
+    for sid, i in sids.items():
+        assert bytes(got[sid]) == bodies[i]
+    # the pool is 1 MiB; beyond it only first buffers (16 KiB) and minimal rings (~33 KiB) per stream
+    assert peak <= (1 << 20) + n * (16 << 10) + n * (34 << 10)
+    hub.close()
+    srv.close()
