@@ -28,6 +28,15 @@ its last one (``object_growth``), naming what grows outside the C heap. With
 ``--out`` the summary so far is rewritten every ``--progress-minutes``
 (``"complete": false``), so a run cut short still leaves its record.
 
+``--api-tls`` puts the API server behind a TLS 1.3 front
+(``testing/tls_front.py``: the native fixture sealer, a KeyUpdate every
+``--key-update-mib`` MiB per connection and a NewSessionTicket every
+``--ticket-every-mib``, half of them cut over two records), so the
+watcher reads its watch over https like production (in-cluster,
+``production.yaml``) through its own TLS record layer; ``--tls`` serves the
+stub clusterapi over https. The front's drops pass the replay fixture's
+aborts on as resets.
+
 Every ``--sample-seconds`` the harness records the watcher's RSS (VmRSS/VmHWM)
 and its gauges: cached pods and cache bytes, owed notifications and bytes,
 checkpoint stall. The sink's keys are handed over and reset every 50 steps
@@ -103,6 +112,19 @@ def rss_segments(samples: List[dict], warmup_minutes: float) -> List[dict]:
     return sorted(out, key=lambda d: -d["minutes"])
 
 
+def tls_by_process(samples: List[dict]) -> List[dict]:
+    """Per watcher process: the TLS record layer's counters at its last
+    sample (streams taken over / left on SSL_read, key updates followed)."""
+    last: Dict[int, dict] = {}
+    for x in samples:
+        if x.get("pid") and x.get("watch_tls_records") is not None:
+            last[x["pid"]] = x
+    return [{"pid": pid, "streams_native": x.get("watch_tls_streams_native"),
+             "streams_openssl": x.get("watch_tls_streams_openssl"), "records": x.get("watch_tls_records"),
+             "key_updates": x.get("watch_tls_key_updates"), "ring_bytes": x.get("watch_reader_tls_ring_bytes")}
+            for pid, x in last.items()]
+
+
 def memory_at_peak(samples: List[dict]) -> Optional[dict]:
     """The highest-RSS sample, broken down by what the watcher reports holding."""
     xs = [x for x in samples if x.get("rss_mb")]
@@ -167,10 +189,15 @@ class Soak:
         self.counts: Dict[int, Dict[str, int]] = {}  # step -> key -> deliveries
         self.verdicts: List[dict] = []
         self.kinds: Dict[int, str] = {}
+        # steps inside a SIGKILL's at-least-once window (the kill step and the
+        # ones the last checkpoint may predate), whatever else they were (a
+        # drop or an expiry there is re-sent too)
+        self.rewound: Set[int] = set()
         self.kills = 0
         self.t0 = time.monotonic()
         self.censuses: List[dict] = []
         self.watcher_started = self.t0
+        self.front = None
 
     # ------------------------------------------------------------------ fixtures
     async def start(self) -> None:
@@ -190,21 +217,36 @@ class Soak:
         spawn = lambda *c: asyncio.create_subprocess_exec(  # noqa: E731
             *c, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
             stderr=asyncio.subprocess.DEVNULL, start_new_session=True, cwd=ROOT)
+        self.pki = None
+        if self.a.api_tls or self.a.tls:
+            from k8s_watcher_amd.testing.certs import make_pki
+            self.pki = make_pki(os.path.join(self.dir, "pki"))
+        sink_tls = ["--tls-cert", self.pki.server_crt, "--tls-key", self.pki.server_key] if self.a.tls else []
         self.replay = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.replay_server",
                                   "--template", "churn", "--pods", str(self.a.pods))
         self.sink = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.stub_sink", "--port",
                                 str(self.sink_port), "--workers", str(self.a.sink_workers),
-                                "--verify-dir", self.verify_dir)
+                                "--verify-dir", self.verify_dir, *sink_tls)
         ready = (await asyncio.wait_for(self.replay.stdout.readline(), 900)).decode().split()
         self.api_port, self.E = int(ready[1]), int(ready[2])
         await self.sink.stdout.readline()
+        self.front = None
+        server = f"http://127.0.0.1:{self.api_port}"
+        if self.a.api_tls:
+            self.front = await spawn(sys.executable, "-m", "k8s_watcher_amd.testing.tls_front",
+                                     "--backend", f"127.0.0.1:{self.api_port}", "--cert", self.pki.server_crt,
+                                     "--key", self.pki.server_key, "--key-update-mib", str(self.a.key_update_mib),
+                                     "--ticket-every-mib", str(self.a.ticket_every_mib))
+            front_port = int((await asyncio.wait_for(self.front.stdout.readline(), 60)).decode().split()[1])
+            server = f"https://127.0.0.1:{front_port}"
+        ca = f", certificate-authority: {self.pki.ca_crt}" if self.a.api_tls else ""
         await asyncio.sleep(0.3)
         cfg = os.path.join(self.dir, "config")
         os.makedirs(cfg)
         with open(os.path.join(self.dir, "kubeconfig"), "w") as fh:
             fh.write(textwrap.dedent(f"""
                 current-context: c
-                clusters: [{{name: c, cluster: {{server: "http://127.0.0.1:{self.api_port}"}}}}]
+                clusters: [{{name: c, cluster: {{server: "{server}"{ca}}}}}]
                 contexts: [{{name: c, context: {{cluster: c, user: u}}}}]
                 users: [{{name: u, user: {{token: x}}}}]
                 """))
@@ -219,16 +261,26 @@ class Soak:
                   retry: {{max_attempts: 0, delay_seconds: 0.1, max_delay_seconds: 2}}
                   checkpoint: {{path: {os.path.join(self.dir, "state", "checkpoint.bin")}, interval_seconds: 5}}
                 """))
+        sink_ca = f"ca_file: {self.pki.ca_crt}, " if self.a.tls else ""
         with open(os.path.join(cfg, "production.yaml"), "w") as fh:
             fh.write(textwrap.dedent(f"""
                 environment: production
-                clusterapi: {{base_url: "http://127.0.0.1:{self.sink_port}", pool: {{connections: 4, pipeline_depth: 32}}}}
+                clusterapi: {{base_url: "{"https" if self.a.tls else "http"}://127.0.0.1:{self.sink_port}", {sink_ca}pool: {{connections: 4, pipeline_depth: 32}}}}
                 watcher:
                   namespaces: [{", ".join(TARGETS)}]
                   log_level: WARNING
                   alerts: {{critical_events_only: true}}
                 """))
         self.cfg = cfg
+
+    async def front_stats(self) -> Optional[dict]:
+        """The TLS front's counters (connections, key updates, tickets, aborts)."""
+        if self.front is None:
+            return None
+        self.front.stdin.write(b"STATS\n")
+        await self.front.stdin.drain()
+        line = (await asyncio.wait_for(self.front.stdout.readline(), 30)).decode()
+        return json.loads(line.split(" ", 1)[1])
 
     async def cmd(self, line: str) -> int:
         self.replay.stdin.write((line + "\n").encode())
@@ -277,7 +329,9 @@ class Soak:
                   "checkpoint_stall_ms", "checkpoint_write_ms", "checkpoint_bytes", "events_received",
                   "notify_delivered", "expired_410", "watch_restarts", "relists", "bookmarks",
                   "apply_partitioned_batches", "apply_partitioned_lines", "apply_tail_serial_lines",
-                  "apply_tail_submits", "apply_tail_lock_runs", "apply_serial_batches", "apply_serial_lines"):
+                  "apply_tail_submits", "apply_tail_lock_runs", "apply_serial_batches", "apply_serial_lines",
+                  "malloc_arenas", "watch_reader_tls_ring_bytes", "watch_tls_streams_native",
+                  "watch_tls_streams_openssl", "watch_tls_records", "watch_tls_key_updates"):
             if k in m:
                 s[k] = m[k]
         self.samples.append(s)
@@ -314,12 +368,12 @@ class Soak:
             seen = {k.split("|")[0] for k in got}
             have_del = {k.split("|")[0] for k in got if "|DELETED|" in k}
             missing = len(seen - have_del)
-            ok = missing == 0 and dups == 0
         else:
             missing = len(want - set(got))
-            ok = missing == 0 and (dups == 0 or kind in ("kill", "pre-kill"))
+        rewound = step in self.rewound
+        ok = missing == 0 and (dups == 0 or rewound)
         self.verdicts.append({"step": step, "kind": kind, "ok": ok, "missing": missing, "duplicates": dups,
-                              "received": sum(got.values())})
+                              "received": sum(got.values()), "rewound": rewound})
 
     async def close(self) -> None:
         if self.watcher is not None and self.watcher.poll() is None:
@@ -328,7 +382,9 @@ class Soak:
                 self.watcher.wait(20)
             except subprocess.TimeoutExpired:
                 os.killpg(self.watcher.pid, signal.SIGKILL)
-        for p in (self.replay, self.sink):
+        for p in (self.replay, self.sink, self.front):
+            if p is None:
+                continue
             try:
                 os.killpg(p.pid, signal.SIGTERM)
             except (ProcessLookupError, PermissionError):
@@ -372,8 +428,10 @@ async def amain(a) -> dict:
                 s.kinds[step] = "kill"
                 # the last checkpoint (every 5 s) may predate these: re-sent after the restart
                 for back in range(1, int(5.0 / a.step_seconds) + 3):
+                    s.rewound.add(step - back)
                     if s.kinds.get(step - back, "normal") == "normal":
                         s.kinds[step - back] = "pre-kill"
+                s.rewound.add(step)
                 send = asyncio.ensure_future(s.cmd(f"STEP {step}"))
                 await asyncio.sleep(a.step_seconds * 0.1)
                 s.sample(step)
@@ -400,6 +458,8 @@ async def amain(a) -> dict:
                     last_sample = time.monotonic()
                     s.sample(step)
                     r = s.samples[-1]
+                    if s.front is not None:
+                        r["front"] = await s.front_stats()
                     print(f"[{r['t']:7.1f}s] step {step} rss {r.get('rss_mb')} MiB cached {r.get('cached_pods')} "
                           f"owed {r.get('notify_outstanding')} ({r.get('notify_outstanding_bytes')} B)",
                           file=sys.stderr, flush=True)
@@ -437,10 +497,13 @@ def summarize(s: "Soak", a, step: int, events: int, complete: bool) -> dict:
         "steps_by_kind": {k: sum(1 for v in s.verdicts if v["kind"] == k)
                           for k in ("normal", "drop", "expire", "kill", "pre-kill")},
         "steps_failed": len(bad), "failed_examples": bad[:5],
-        "duplicates_outside_kill_steps": sum(v["duplicates"] for v in s.verdicts
-                                             if v["kind"] not in ("kill", "pre-kill")),
-        "duplicates_in_kill_steps": sum(v["duplicates"] for v in s.verdicts if v["kind"] in ("kill", "pre-kill")),
+        "duplicates_outside_kill_steps": sum(v["duplicates"] for v in s.verdicts if not v.get("rewound")),
+        "duplicates_in_kill_steps": sum(v["duplicates"] for v in s.verdicts if v.get("rewound")),
         "notifications_checked": sum(v["received"] for v in s.verdicts),
+        "transport": {"api_server": "https" if a.api_tls else "http", "clusterapi": "https" if a.tls else "http",
+                      "key_update_mib": a.key_update_mib if a.api_tls else None,
+                      "front": next((x["front"] for x in reversed(s.samples) if x.get("front")), None),
+                      "watcher_key_updates_by_process": tls_by_process(s.samples)},
         "rss_mb_after_warmup": {"min": min(x["rss_mb"] for x in after) if after else None,
                                 "max": max(x["rss_mb"] for x in after) if after else None,
                                 "slope_mib_per_hour": slope_mib_per_hour([(x["t"], x["rss_mb"]) for x in after])},
@@ -470,6 +533,13 @@ def main(argv=None) -> int:
                     help="run the watcher without PYTHONTRACEMALLOC (object counts only)")
     ap.add_argument("--progress-minutes", type=float, default=15.0,
                     help="with --out: rewrite the summary so far this often")
+    ap.add_argument("--api-tls", action="store_true",
+                    help="the API server over https (TLS front with key updates): production's transport")
+    ap.add_argument("--tls", action="store_true", help="the stub clusterapi over https")
+    ap.add_argument("--key-update-mib", type=float, default=64.0,
+                    help="with --api-tls: a KeyUpdate every N MiB on each connection")
+    ap.add_argument("--ticket-every-mib", type=float, default=256.0,
+                    help="with --api-tls: a NewSessionTicket every N MiB on each connection")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     res = asyncio.run(amain(a))

@@ -341,6 +341,13 @@ class WatcherService:
                 self.metrics.gauges["watch_reader_allocated_bytes"] = \
                     lambda: float(hub.stats().get("allocated_bytes", 0))
                 self.metrics.gauges["watch_reader_held_bytes"] = lambda: float(hub.stats().get("held_bytes", 0))
+                # https watches on the hub's own TLS 1.3 record layer (ops/csrc/tls13.inc):
+                # ciphertext rings (inside watch_reader_allocated_bytes), streams taken
+                # over / left on SSL_read, records opened and key updates followed
+                for key, name in (("tls_ring_bytes", "watch_reader_tls_ring_bytes"),
+                                  ("tls_taken", "watch_tls_streams_native"), ("tls_kept", "watch_tls_streams_openssl"),
+                                  ("tls_records", "watch_tls_records"), ("tls_key_updates", "watch_tls_key_updates")):
+                    self.metrics.gauges[name] = lambda key=key: float(hub.stats().get(key, 0))
             self._pin_threads()
         if owed:
             # the checkpoint's cut: clusterapi never acknowledged these; send them
@@ -365,6 +372,7 @@ class WatcherService:
             _mi = _load_native().malloc_info
             self.metrics.gauges["malloc_in_use_bytes"] = lambda: float(_mi()["in_use_bytes"])
             self.metrics.gauges["malloc_free_bytes"] = lambda: float(_mi()["free_bytes"])
+            self.metrics.gauges["malloc_arenas"] = lambda: float(len(_load_native().malloc_arenas()))
         self.metrics.gauges["notify_outstanding"] = lambda: float(self.notifier.outstanding())
         if hasattr(self.notifier, "outstanding_bytes"):
             self.metrics.gauges["notify_outstanding_bytes"] = lambda: float(self.notifier.outstanding_bytes())

@@ -251,6 +251,12 @@ def memory_census(top: int = 40) -> Dict[str, object]:
         "gc_objects": sum(counts.values()), "garbage_collected": collected, "frozen_before": frozen,
         "allocated_blocks": sys.getallocatedblocks(),
         "types": dict(sorted(counts.items(), key=lambda kv: -kv[1])[:top]), "gc_counts": list(gc.get_count())}
+    try:  # the C heap per glibc arena (0: main, the loop's): where retained free bytes sit
+        from .ops.native import load as _load_native
+        out["malloc_arenas"] = [{"arena": a, "free_bytes": f, "system_bytes": sz}
+                                for a, f, sz in _load_native().malloc_arenas()]
+    except Exception:  # noqa: BLE001 - no native extension (python engine): not part of the census
+        pass
     if tracemalloc.is_tracing():
         snap = tracemalloc.take_snapshot().filter_traces(
             [tracemalloc.Filter(False, tracemalloc.__file__)])

@@ -2097,6 +2097,50 @@ PyObject* kw_malloc_info(PyObject*, PyObject*) {
                          (Py_ssize_t)mi.hblkhd);
 }
 
+// malloc_arenas() -> [(arena, free_bytes, system_bytes)]: glibc's
+// malloc_info() per arena (0 is the main arena, the event loop's; the others
+// belong to native threads) — where the retained free bytes of the C heap sit
+// (soak attribution: benchmarks/soak.py samples it).
+PyObject* kw_malloc_arenas(PyObject*, PyObject*) {
+    char* buf = nullptr;
+    size_t len = 0;
+    FILE* f = open_memstream(&buf, &len);
+    if (!f) return PyErr_SetFromErrno(PyExc_OSError);
+    malloc_info(0, f);
+    std::fclose(f);
+    std::string xml(buf ? buf : "", len);
+    std::free(buf);
+    PyObject* out = PyList_New(0);
+    if (!out) return nullptr;
+    auto attr = [](const std::string& x, size_t from, size_t to, const char* tag, const char* key) -> long long {
+        const size_t t = x.find(tag, from);
+        if (t == std::string::npos || t >= to) return 0;
+        const size_t k = x.find(key, t);
+        if (k == std::string::npos || k >= to) return 0;
+        return std::atoll(x.c_str() + k + std::strlen(key));
+    };
+    size_t pos = 0;
+    for (;;) {
+        const size_t h = xml.find("<heap nr=\"", pos);
+        if (h == std::string::npos) break;
+        const size_t e = xml.find("</heap>", h);
+        if (e == std::string::npos) break;
+        const int nr = std::atoi(xml.c_str() + h + 10);
+        const long long fr = attr(xml, h, e, "<total type=\"fast\"", "size=\"") +
+                             attr(xml, h, e, "<total type=\"rest\"", "size=\"");
+        const long long sys = attr(xml, h, e, "<system type=\"current\"", "size=\"");
+        PyObject* t = Py_BuildValue("(iLL)", nr, fr, sys);
+        if (!t || PyList_Append(out, t) < 0) {
+            Py_XDECREF(t);
+            Py_DECREF(out);
+            return nullptr;
+        }
+        Py_DECREF(t);
+        pos = e;
+    }
+    return out;
+}
+
 // malloc_trim() -> bool: give the C heap's free pages back to the kernel
 // (every arena; the decode workers' arenas keep what their threads freed).
 // Runs without the GIL: the service calls it from an executor thread.
@@ -2110,6 +2154,8 @@ PyObject* kw_malloc_trim(PyObject*, PyObject*) {
 
 PyMethodDef module_methods[] = {
     {"malloc_trim", (PyCFunction)kw_malloc_trim, METH_NOARGS, "malloc_trim() -> released (glibc malloc_trim(0), no GIL)"},
+    {"malloc_arenas", (PyCFunction)kw_malloc_arenas, METH_NOARGS,
+     "malloc_arenas() -> [(arena, free_bytes, system_bytes)] (glibc malloc_info per arena)"},
     {"malloc_info", (PyCFunction)kw_malloc_info, METH_NOARGS,
      "malloc_info() -> {in_use_bytes, free_bytes, arena_bytes, mmap_bytes} (glibc mallinfo2)"},
     {"json_invalid", (PyCFunction)kw_json_invalid, METH_O, "json_invalid(data) -> None | reason (json.loads semantics)"},

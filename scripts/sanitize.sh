@@ -2,8 +2,8 @@
 # Host-code sanitizer runs of the native extension (_kwcore), SURVEY §5.2:
 #  * ASan + UBSan over every test that drives the C++ decoder, pipeline,
 #    pod cache and notifier core;
-#  * TSan over the tests that run the decode worker pool (DecodePool) and the
-#    end-to-end service.
+#  * TSan over the tests that run the decode worker pool (DecodePool), the
+#    end-to-end service and the TLS record layer's CryptoPool / writer threads.
 # The interpreter is not instrumented: the sanitizer runtime is preloaded and
 # the instrumented build is loaded via $K8S_WATCHER_KWCORE_SO (ops/native.py).
 # Never run on the GPU box (GPU sanitizers are not available there; this is
@@ -22,7 +22,7 @@ ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print
   tests/test_native_parity.py tests/test_native_pipeline.py tests/test_podcache.py tests/test_notifier.py \
   tests/test_spool.py tests/test_notifier_tls.py tests/test_watch_list.py tests/test_e2e_slice.py tests/test_reflector.py tests/test_http_metrics.py tests/test_reader_hub.py tests/test_reader_hub_tls.py tests/test_native_sink.py \
   tests/test_validate.py tests/test_pyrepr.py tests/test_native_relist.py tests/test_relist_storm.py tests/test_memory.py \
-  tests/test_partitioned_apply.py tests/test_cluster_replay.py \
+  tests/test_partitioned_apply.py tests/test_cluster_replay.py tests/test_tls13.py \
   2>&1 | tee build/asan.log | tail -3
 echo "== TSan"
 K8S_WATCHER_KWCORE_SO=build/sanitize-thread/$SO \
@@ -31,7 +31,7 @@ LD_PRELOAD="$(g++ -print-file-name=libtsan.so)" TSAN_OPTIONS=report_signal_unsaf
   tests/test_native_pipeline.py tests/test_e2e_slice.py tests/test_reflector.py tests/test_native_parity.py \
   tests/test_notifier.py tests/test_notifier_tls.py tests/test_spool.py tests/test_leader.py tests/test_reader_hub.py tests/test_reader_hub_tls.py tests/test_native_sink.py \
   tests/test_sharding.py::test_discover_scope_two_shards_exactly_once tests/test_sharding.py::test_deleted_namespace_drains_then_synthesizes_deleted \
-  tests/test_native_relist.py tests/test_relist_storm.py tests/test_partitioned_apply.py \
+  tests/test_native_relist.py tests/test_relist_storm.py tests/test_partitioned_apply.py tests/test_tls13.py \
   2>&1 | tee build/tsan.log | tail -3
 if grep -q "WARNING: ThreadSanitizer\|ERROR: AddressSanitizer\|runtime error:" build/asan.log build/tsan.log; then
   echo "sanitizer reports found (build/asan.log, build/tsan.log)"; exit 1
