@@ -40,7 +40,7 @@ from ..ops.cache import CORE, NAME, NS, PHASE, RV, make_pod_cache
 from ..ops.decode import make_decoder
 from ..parallel.native_notifier import NativeNotifierPool
 from ..parallel.notifier import NotifierPool, NullNotifier
-from ..parallel.shard import ShardFilter, owner_of, take_handover, write_handover
+from ..parallel.shard import ShardFilter, layout_of, owner_of, record_layout, take_handover, write_handover
 from ..parallel.spool import Spool, SpoolReplayer
 from ..utils.config import Settings
 from ..utils.fastlog import EventLog
@@ -113,6 +113,10 @@ class WatcherService:
         # namespaces gained from another shard, waiting for its hand-over record
         # before their watch starts (watcher.shard.handover_dir)
         self._gaining: Dict[str, asyncio.Task] = {}
+        # namespaces handed to another shard whose record waits for this shard's
+        # owed notifications of them to be acknowledged (_handover_out)
+        self._handing: Dict[str, asyncio.Task] = {}
+        self._layout_since = 0.0  # when the shard layout in handover_dir's history began (record_layout)
         self._ns_seen: Set[str] = set()  # the namespace set the last ownership decision used
         self._retiring: Dict[str, asyncio.TimerHandle] = {}  # deleted namespaces draining their pod watch
         self._failure: Optional[asyncio.Future] = None
@@ -349,6 +353,9 @@ class WatcherService:
                                   ("tls_records", "watch_tls_records"), ("tls_key_updates", "watch_tls_key_updates")):
                     self.metrics.gauges[name] = lambda key=key: float(hub.stats().get(key, 0))
             self._pin_threads()
+        gains: Set[str] = set()
+        if s.watcher.shard.handover_dir and self._multi and s.watcher.shard.key == "namespace":
+            gains, owed = self._reshard_on_start(scopes, saved_rvs, owed)
         if owed:
             # the checkpoint's cut: clusterapi never acknowledged these; send them
             # (in their original order) before anything newer — the watches that
@@ -383,7 +390,10 @@ class WatcherService:
         else:
             self.log.info("Monitoring all namespaces")
         for i, ns in enumerate(scopes):
-            self._start_scope(ns, primed=bool(saved_rvs))
+            if ns in gains:  # another shard's under the previous layout: its record first
+                self._gain_scope(ns)
+            else:
+                self._start_scope(ns, primed=bool(saved_rvs))
             if i % 64 == 63:  # a thousand namespaces: let the started scopes (and the loop) run meanwhile
                 await asyncio.sleep(0)
                 if self._stop.is_set():
@@ -466,59 +476,156 @@ class WatcherService:
         if task is not None and not task.done():
             task.cancel()
         if handover_to is not None and stopped:
-            self._handover_out(ns, handover_to)
+            # the namespace's pods stay cached until the record is written
+            self._handing[ns] = asyncio.ensure_future(self._handover_out(ns, handover_to))
+            return
         self._forget_namespaces({ns})
 
-    def _handover_out(self, ns: str, dst: int) -> None:
-        """The old owner's half of a namespace hand-over: with its watch
-        stopped, this shard's cached pods of ``ns`` go to the shared
-        directory for shard ``dst`` (parallel/shard.py)."""
+    def _cached_pods_of(self, cache, ns: str) -> list:
+        return [(uid, e[RV], e[PHASE], e[NAME], e[CORE]) for uid, e in cache.items() if e[NS] == ns]
+
+    async def _handover_out(self, ns: str, dst: int) -> None:
+        """The old owner's half of a live namespace hand-over: with its watch
+        stopped, wait until clusterapi has acknowledged (or this shard has
+        given up) every notification still owed for the namespace — a retried
+        MODIFIED (clusterapi answering 503, say) must not land after the new
+        owner's notifications for the same pod — then write this shard's
+        cached pods of ``ns`` to the shared directory for shard ``dst``
+        (parallel/shard.py) and forget them. The wait is bounded by half of
+        ``shard.handover_wait_seconds`` (the new owner's patience): past it the
+        record goes out anyway and the late notifications are counted
+        (``shard_handover_owed_late``)."""
         sh = self.settings.watcher.shard
-        cache = self.pipeline.cache if self.pipeline is not None else None
-        if cache is None:
-            return
-        pods = [(uid, e[RV], e[PHASE], e[NAME], e[CORE]) for uid, e in cache.items() if e[NS] == ns]
+        loop = asyncio.get_running_loop()
         try:
-            write_handover(sh.handover_dir, ns, sh.index, dst, pods)
+            deadline = loop.time() + sh.handover_wait_seconds / 2
+            pending_in = getattr(self.notifier, "pending_in", None)
+            late = 0
+            while pending_in is not None and not self._stop.is_set():
+                late = pending_in(ns)
+                if late == 0 or loop.time() >= deadline:
+                    break
+                await asyncio.sleep(0.05)
+            if late:
+                self.metrics.c["shard_handover_owed_late"] += late
+                self.log.warning(f"Handing namespace {ns} over with {late} notification(s) for it still owed "
+                                 f"to clusterapi: they may arrive after shard {dst}'s")
+            cache = self.pipeline.cache if self.pipeline is not None else None
+            if cache is None:
+                return
+            pods = self._cached_pods_of(cache, ns)
+            try:
+                # (json + fsync on a shared volume: off the loop)
+                await loop.run_in_executor(None, write_handover, sh.handover_dir, ns, sh.index, dst, pods, None,
+                                           layout_of(sh))
+            except OSError as exc:
+                self.metrics.c["shard_handover_errors"] += 1
+                self.log.error(f"Could not write the hand-over of namespace {ns} to shard {dst} "
+                               f"({exc}): its new owner will re-announce its pods")
+            else:
+                self.metrics.c["shard_handovers_out"] += 1
+                self.metrics.c["shard_handover_pods_out"] += len(pods)
+                self.log.info(f"Handed namespace {ns} ({len(pods)} cached pods) over to shard {dst}")
+            if self._handing.get(ns) is asyncio.current_task():
+                self._forget_namespaces({ns})
+        finally:
+            if self._handing.get(ns) is asyncio.current_task():
+                del self._handing[ns]
+
+    def _reshard_on_start(self, scopes, saved_rvs: dict, owed: list):
+        """A new shard layout (``shard.count`` changed, every shard restarted):
+        the hand-over across a restart (parallel/shard.py). Notes the layout in
+        ``handover_dir``'s history, writes a record for every namespace this
+        shard held (its checkpoint) or owned under the previous layout that
+        another shard owns now — with the checkpoint's owed notifications for
+        it, which then are not re-sent here — and returns the namespaces this
+        shard now owns that were another's, which wait for their record.
+        Returns ``(gains, owed left to re-send here)``."""
+        sh = self.settings.watcher.shard
+        layout = layout_of(sh)
+        try:
+            prev, self._layout_since = record_layout(sh.handover_dir, layout)
         except OSError as exc:
-            self.metrics.c["shard_handover_errors"] += 1
-            self.log.error(f"Could not write the hand-over of namespace {ns} to shard {dst} "
-                           f"({exc}): its new owner will re-announce its pods")
-            return
-        self.metrics.c["shard_handovers_out"] += 1
-        self.metrics.c["shard_handover_pods_out"] += len(pods)
-        self.log.info(f"Handed namespace {ns} ({len(pods)} cached pods) over to shard {dst}")
+            self.log.error(f"Could not record the shard layout in {sh.handover_dir} ({exc}): no hand-over")
+            return set(), owed
+        if self.ns_watcher is not None:
+            names = set(self._ns_seen)
+        else:
+            names = set(self.settings.watcher.namespaces)
+        owned = {x for x in scopes if x}
+        cache = self.pipeline.cache
+        held = {ns for ns in cache.namespaces() if ns is not None} | {k for k in saved_rvs if k != "*"}
+        was_mine = set()
+        if prev and prev != layout and prev.get("key", "namespace") == "namespace":
+            was_mine = {ns for ns in names if owner_of(ns, names, prev["count"], prev["assignment"]) == sh.index}
+        out = sorted(ns for ns in (held | was_mine) if ns in names and ns not in owned)
+        for ns in out:
+            dst = owner_of(ns, names, sh.count, sh.assignment)
+            pods = self._cached_pods_of(cache, ns)
+            mine = [o for o in owed if o[2] == ns]
+            try:
+                write_handover(sh.handover_dir, ns, sh.index, dst, pods, mine, layout)
+            except OSError as exc:
+                self.metrics.c["shard_handover_errors"] += 1
+                self.log.error(f"Could not write the hand-over of namespace {ns} to shard {dst} ({exc})")
+                continue
+            self.metrics.c["shard_handovers_out"] += 1
+            self.metrics.c["shard_handover_pods_out"] += len(pods)
+            self.log.info(f"New shard layout {layout}: handed namespace {ns} ({len(pods)} cached pods, "
+                          f"{len(mine)} owed notifications) over to shard {dst}")
+        gone = set(out)
+        owed = [o for o in owed if o[2] not in gone]
+        gains: Set[str] = set()
+        if prev and prev != layout and prev.get("key", "namespace") == "namespace":
+            gains = {ns for ns in owned if ns not in saved_rvs
+                     and owner_of(ns, names, prev["count"], prev["assignment"]) != sh.index}
+            if gains:
+                self.log.info(f"New shard layout {layout} (was {prev}): waiting for the hand-over of "
+                              f"{len(gains)} namespace(s) from their old owners")
+        return gains, owed
 
     def _gain_scope(self, ns: str) -> None:
         self._gaining[ns] = asyncio.ensure_future(self._await_handover(ns))
 
     async def _await_handover(self, ns: str) -> None:
-        """The new owner's half: wait for the old owner's record, load it into
-        the cache, then start the watch — its first LIST reconciles against
-        that state (unchanged pods stay quiet, pods gone meanwhile are
-        DELETED), as a relist after a 410 would."""
+        """The new owner's half: wait for the old owner's record, send the
+        notifications it still owed for the namespace (before anything of this
+        shard's), load its pods into the cache, then start the watch — its
+        first LIST reconciles against that state (unchanged pods stay quiet,
+        pods gone meanwhile are DELETED), as a relist after a 410 would.
+        Records written before this wait could have been meant for it (an
+        older move's, whose new owner timed out) or under another layout are
+        stale and discarded."""
         sh = self.settings.watcher.shard
         loop = asyncio.get_running_loop()
         deadline = loop.time() + sh.handover_wait_seconds
+        # a live move's record is written after the old owner saw the change
+        # (seconds around ours); a restart's since the layout began
+        not_before = min(time.time() - max(60.0, sh.handover_wait_seconds),
+                         self._layout_since - 60.0 if self._layout_since else time.time())
+        layout = layout_of(sh)
         while True:
-            pods = take_handover(sh.handover_dir, ns, sh.index)
-            if pods is not None or loop.time() >= deadline or self._stop.is_set():
+            rec = take_handover(sh.handover_dir, ns, sh.index, not_before=not_before, layout=layout)
+            if rec is not None or loop.time() >= deadline or self._stop.is_set():
                 break
             await asyncio.sleep(0.05)
         if self._gaining.get(ns) is not asyncio.current_task() or self._stop.is_set():
             return
         del self._gaining[ns]
-        if pods is None:
+        if rec is None:
             self.metrics.c["shard_handover_timeouts"] += 1
             self.log.warning(f"No hand-over of namespace {ns} from its old owner after "
                              f"{sh.handover_wait_seconds}s: its pods are announced as ADDED again")
         else:
+            if rec.owed:  # the old owner's unacknowledged notifications: first, in their order
+                self._resubmit_owed(list(rec.owed))
             cache = self.pipeline.cache
-            for uid, rv, phase, name, core in pods:
+            for uid, rv, phase, name, core in rec.pods:
                 cache.put(uid, rv, phase, ns, name, core)
             self.metrics.c["shard_handovers_in"] += 1
-            self.metrics.c["shard_handover_pods_in"] += len(pods)
-            self.log.info(f"Took over namespace {ns} ({len(pods)} pods from its old owner)")
+            self.metrics.c["shard_handover_pods_in"] += len(rec.pods)
+            self.log.info(f"Took over namespace {ns} ({len(rec.pods)} pods, {len(rec.owed)} owed "
+                          f"notifications from shard {rec.src})")
         self._start_scope(ns, primed=True)
 
     def _forget_namespaces(self, namespaces: Set[str]) -> None:
@@ -565,6 +672,9 @@ class WatcherService:
         for ns in sorted(owned & set(self._retiring)):  # deleted and created again: keep watching
             self._retiring.pop(ns).cancel()
         for ns in sorted(owned - current):
+            handing = self._handing.pop(ns, None)
+            if handing is not None:  # back before its record went out: still ours, cache and all
+                handing.cancel()
             self.metrics.c["scopes_started"] += 1
             self.log.info(f"Watching namespace {ns} (new or now owned by shard {sh.index})")
             if sh.handover_dir and ns in prev and owner_of(ns, prev, sh.count, sh.assignment) != sh.index:
@@ -754,6 +864,9 @@ class WatcherService:
             self.ns_watcher.stop()
         for r in self.reflectors:
             r.stop()
+        for t in self._handing.values():  # records not written yet: their pods stay in the checkpoint,
+            t.cancel()                    # and the restart hands them over (_reshard_on_start)
+        self._handing.clear()
         drained = True
         closed = False
         if self.notifier is not None:

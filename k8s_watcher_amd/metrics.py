@@ -68,6 +68,7 @@ COUNTERS = (
     "shard_handover_pods_in",
     "shard_handover_timeouts",  # a moved namespace's record never came (its pods re-announced)
     "shard_handover_errors",    # a record could not be written
+    "shard_handover_owed_late",  # notifications still owed for a namespace when its record went out anyway
     "notify_io_switches",   # clusterapi.pool.io_thread: auto — sockets handed between loop and I/O thread
     "namespace_deleted_synthesized",  # pods of a deleted namespace notified DELETED from the cache (no event came)
     "leader_acquired",      # leadership terms started (engine/leader.py)

@@ -162,6 +162,10 @@ class NativeNotifierPool:
     def outstanding(self) -> int:
         return self.core.pending()
 
+    def pending_in(self, namespace: str) -> int:
+        """Outstanding notifications (queued, in flight, retrying) for pods of ``namespace``."""
+        return self.core.pending_in(namespace)
+
     def outstanding_bytes(self) -> int:
         return self.core.pending_bytes()
 

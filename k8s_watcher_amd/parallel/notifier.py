@@ -447,6 +447,13 @@ class NotifierPool:
     def outstanding_bytes(self) -> int:
         return self.pending_bytes
 
+    def pending_in(self, namespace: str) -> int:
+        """Outstanding notifications (queued, in flight, retrying) for pods of ``namespace``."""
+        n = sum(1 for r in self.retrying.values() if r.ns == namespace)
+        for c in self.conns:
+            n += sum(1 for r in c.inflight if r.ns == namespace) + sum(1 for r in c.queue if r.ns == namespace)
+        return n
+
     # ------------------------------------------------------------------ bookkeeping
     def _add_pending(self, n: int, nbytes: int = 0) -> None:
         self.pending += n
@@ -568,4 +575,7 @@ class NullNotifier:
         pass
 
     def outstanding(self) -> int:
+        return 0
+
+    def pending_in(self, namespace: str) -> int:
         return 0
