@@ -47,8 +47,10 @@ def _drain(hub, sid, timeout=30.0):
     got, end = bytearray(), None
     t_end = time.monotonic() + timeout
     while end is None and time.monotonic() < t_end:
-        for s, buf, view, _ns, err in hub.take():
+        for s, buf, view, ns, err in hub.take():
             assert s == sid
+            if view is not None:
+                assert ns > 0  # a batch received ahead (the overlap) still has its arrival time
             if view is None:
                 end = err
             else:
