@@ -86,6 +86,9 @@ def parse_args(argv=None):
                     help="also run the staging profile (every event notified): its saturated notification rate "
                          "and p50/p99 at --staging-latency-rate (auto: after a production run)")
     ap.add_argument("--staging-steps", type=int, default=4, help="timed steps of the staging phase")
+    ap.add_argument("--full-validate-steps", type=int, default=4,
+                    help="after the headline: timed steps of the same replay with watcher.validate: full "
+                         "(every byte JSON-checked, as the reference's json.loads of every event); 0 = skip")
     ap.add_argument("--staging-latency-rate", type=float, default=100000.0,
                     help="ev/s over the whole job for the staging phase's latency figure")
     ap.add_argument("--soak-minutes", type=float, default=0.0,
@@ -1512,6 +1515,30 @@ def main(argv=None) -> int:
                  "exactly_once": (v2["duplicates"] == 0 and v2["unique"] == r2["notifiable"]
                                   and v2["received"] == r2["notifiable"]) if v2 else None,
                  "placement_rank0": r2["placement"]}
+    full = None
+    if args.full_validate_steps > 0 and (args.validate or "payload") != "full" and args.engine == "native":
+        # the headline's work level named: watcher.validate: payload checks the
+        # bytes copied into payloads (JSON the watcher forwards), the reference
+        # json.loads every event byte (pod_watcher.py:264) — the same replay
+        # with every byte validated, for the rate at the reference's level
+        import copy
+        a4 = copy.copy(args)
+        a4.validate = "full"
+        a4.latency_seconds = a4.latency_seconds_high = 0.0
+        a4.ref_events = 0
+        a4.probe = False
+        a4.warmup = 1
+        a4.steps = args.full_validate_steps
+        progress(d, "validate: full (every byte checked)")
+        r4 = asyncio.run(rank_main(a4, d))
+        el4 = d.reduce(r4["elapsed"], "MAX")
+        ev4 = d.reduce(float(r4["events"]), "SUM")
+        v4 = r4["verify"]
+        full = {"validate": "full", "value": round(ev4 / el4, 1), "steps": a4.steps, "warmup": a4.warmup,
+                "ms_per_step": round(el4 / a4.steps * 1000, 3), "rate_series": _series_stats(
+                    _sum_series(d.all_gather(r4["series"]))),
+                "exactly_once": (v4["duplicates"] == 0 and v4["unique"] == r4["notifiable"]
+                                 and v4["received"] == r4["notifiable"]) if v4 else None}
     staging = None
     if args.staging == "on" or (args.staging == "auto" and args.profile == "production"):
         # BASELINE configs #2/#3: every event notified (the staging profile) —
@@ -1626,6 +1653,7 @@ def main(argv=None) -> int:
         "malloc_trim_rank0": res["trims"],
         "rss_mib_rank0": ({"first": rss[0][0], "last": rss[0][-1], "max": max(rss[0])} if rss and rss[0] else None),
         "placement_apart": apart,
+        "validate_full": full,
         "staging": staging,
         "gc_rank0": res["gc"],
         "notified_per_s": round(notified / elapsed, 1),
@@ -1691,7 +1719,7 @@ def headline(o: dict, path: str) -> dict:
     h = {k: o[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "timed_seconds",
                            "higher_is_better", "scaling", "vs_baseline", "dtype", "data")}
     h["config"] = {k: cfg[k] for k in ("model", "global_batch", "seq_len", "parallelism", "api_server", "clusterapi",
-                                       "namespaces", "target_namespaces")}
+                                       "namespaces", "target_namespaces", "engine", "validate", "state_format")}
     h["p50_latency_ms"] = o["p50_latency_ms"]
     h["p99_latency_ms"] = o["p99_latency_ms"]
     h["latency_rate_ev_s_per_rank"] = o["latency_rate_ev_s_per_rank"]
@@ -1707,6 +1735,8 @@ def headline(o: dict, path: str) -> dict:
     h["staging"] = ({"notified_per_s": st["every_event_notified_per_s"], "p50_ms": st["p50_latency_ms"],
                      "p99_ms": st["p99_latency_ms"], "exactly_once": st["exactly_once"]} if st else None)
     h["placement_apart"] = {"value": ap["value"], "exactly_once": ap["exactly_once"]} if ap else None
+    vf = o.get("validate_full")
+    h["validate_full"] = {"value": vf["value"], "exactly_once": vf["exactly_once"]} if vf else None
     h["detail_json"] = path
     return h
 

@@ -30,7 +30,7 @@ BASELINE = json.load(open(os.path.join(ROOT, "BASELINE.json")))
 HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "timed_seconds",
                  "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "p50_latency_ms",
                  "p99_latency_ms", "latency_1k", "loop_lag_1k", "rate_series", "exactly_once",
-                 "reference_equiv_events_per_s", "staging", "placement_apart", "detail_json")
+                 "reference_equiv_events_per_s", "staging", "placement_apart", "validate_full", "detail_json")
 
 
 def tagged_processes(tag: str) -> list:
@@ -75,6 +75,10 @@ def check_headline(proc, out, left):
     assert head["value"] > 0 and head["higher_is_better"] is True and head["scaling"] == "weak"
     assert head["exactly_once"] is True and head["notify_failed"] == 0
     assert head["staging"]["exactly_once"] and head["placement_apart"]["exactly_once"]
+    # the headline's work level is named, with the rate at the reference's (every byte JSON-checked)
+    assert {head["config"][k] for k in ("engine", "validate", "state_format")} == {"native", "payload", "structured"}
+    assert head["validate_full"]["exactly_once"] and head["validate_full"]["value"] > 0
+    assert d["validate_full"]["validate"] == "full"
     assert head["reference_equiv_events_per_s"] > 0 and head["vs_baseline"] > 0
     assert head["p50_latency_ms"] > 0 and head["latency_1k"]["p99_ms"] >= head["latency_1k"]["p50_ms"] > 0
     lag = head["loop_lag_1k"]
