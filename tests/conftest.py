@@ -12,6 +12,7 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs the MI355X box (run with -m gpu)")
     config.addinivalue_line("markers", "slow: long-running soak/bench style test")
+    config.addinivalue_line("markers", "perf: wall-clock rate comparison (box tier only: also marked gpu)")
 
 
 @pytest.fixture(scope="session", autouse=True)

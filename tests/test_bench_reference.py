@@ -10,7 +10,13 @@ starts at the first paced event."""
 
 import os
 
+import pytest
+
 from conftest import run_bench  # noqa: E402
+
+# a wall-clock rate comparison: a noise gate on a shared container, so it runs
+# in the box's tier (-m gpu; the host's own CPU share) and not the CPU tier
+pytestmark = [pytest.mark.gpu, pytest.mark.perf]
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
