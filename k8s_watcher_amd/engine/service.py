@@ -237,6 +237,13 @@ class WatcherService:
             # per doubling on a 256-CPU host (utils/fds.py)
             from ..utils.fds import reserve_fd_table
             reserve_fd_table(s.watcher.fd_table_reserve)
+        if self._native_pipeline() and s.watcher.malloc_trim_seconds > 0:
+            # fixed glibc thresholds before the cache and the buffers exist:
+            # blocks >= 512 KiB on their own mappings (unmapped when freed),
+            # so multi-MiB transients leave no holes in the arenas (round-5
+            # soak: RSS grew with retained free bytes; kwcore.cpp malloc_tune)
+            from ..ops.native import load as _load_kw
+            _load_kw().malloc_tune(512 << 10, 4 << 20)
         if s.watcher.gc_freeze and gc.get_freeze_count() == 0:
             # what import and configuration made is permanent: the full
             # collections that starting a thousand scopes triggers then walk

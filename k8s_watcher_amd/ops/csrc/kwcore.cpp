@@ -2152,7 +2152,29 @@ PyObject* kw_malloc_trim(PyObject*, PyObject*) {
     return PyBool_FromLong(r);
 }
 
+// malloc_tune(mmap_threshold, trim_threshold) -> bool: fixed glibc thresholds.
+// Left dynamic, glibc raises its mmap threshold to the size of every large
+// block freed (up to 32 MiB), so after one 4 MiB read buffer or relist batch
+// goes, later multi-MiB transients are carved from the arenas between
+// long-lived chunks and what they free stays there as holes that neither
+// trimming nor malloc_trim can return (round-5 soak: RSS +12 MiB, all of it
+// retained free bytes). A fixed threshold keeps every block at or above it
+// on its own mapping, unmapped when freed. Process-wide; call once at start.
+PyObject* kw_malloc_tune(PyObject*, PyObject* args) {
+    Py_ssize_t mmap_thr = 0, trim_thr = 0;
+    if (!PyArg_ParseTuple(args, "nn", &mmap_thr, &trim_thr)) return nullptr;
+    if (mmap_thr <= 0 || trim_thr <= 0 || mmap_thr > (Py_ssize_t)(32 << 20) || trim_thr > ((Py_ssize_t)1 << 30)) {
+        PyErr_SetString(PyExc_ValueError, "malloc_tune: thresholds out of range");
+        return nullptr;
+    }
+    const int a = mallopt(M_MMAP_THRESHOLD, (int)mmap_thr);
+    const int b = mallopt(M_TRIM_THRESHOLD, (int)trim_thr);
+    return PyBool_FromLong(a == 1 && b == 1);
+}
+
 PyMethodDef module_methods[] = {
+    {"malloc_tune", (PyCFunction)kw_malloc_tune, METH_VARARGS,
+     "malloc_tune(mmap_threshold, trim_threshold) -> ok (glibc mallopt; fixes both, disabling their sliding)"},
     {"malloc_trim", (PyCFunction)kw_malloc_trim, METH_NOARGS, "malloc_trim() -> released (glibc malloc_trim(0), no GIL)"},
     {"malloc_arenas", (PyCFunction)kw_malloc_arenas, METH_NOARGS,
      "malloc_arenas() -> [(arena, free_bytes, system_bytes)] (glibc malloc_info per arena)"},

@@ -90,3 +90,43 @@ def test_service_defers_trim_under_load():
 
     m = asyncio.run(body())
     assert m.c.get("malloc_trims", 0) == 0 and m.c["malloc_trims_deferred"] >= 1
+
+
+_TUNE_PROBE = r"""
+import sys
+from k8s_watcher_amd.ops.native import load
+kw = load()
+if sys.argv[1] == "tune":
+    assert kw.malloc_tune(512 << 10, 4 << 20) is True
+big = bytearray(8 << 20)  # freed: a sliding threshold would rise to 8 MiB
+del big
+held = bytearray(1 << 20)  # 1 MiB: its own mapping only under a fixed threshold
+print(kw.malloc_info()["mmap_bytes"])
+"""
+
+
+@pytest.mark.parametrize("mode", ["tune", "default"])
+def test_malloc_tune_keeps_transients_off_the_arenas(mode):
+    """kwcore.malloc_tune fixes glibc's mmap threshold: after an 8 MiB block
+    is freed, a 1 MiB block still gets its own mapping (returned to the kernel
+    when freed) instead of a hole in the arena; glibc's default slides the
+    threshold up to 8 MiB and carves the 1 MiB block from the heap."""
+    import subprocess
+    import sys
+    if "asan" in os.environ.get("LD_PRELOAD", ""):
+        pytest.skip("the sanitizer replaced glibc's allocator")
+    out = subprocess.run([sys.executable, "-c", _TUNE_PROBE, mode], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    mmapped = int(out.stdout.split()[-1])
+    if mode == "tune":
+        assert mmapped >= 1 << 20
+    else:
+        assert mmapped < 1 << 20
+
+
+def test_malloc_tune_rejects_out_of_range():
+    kw = load()
+    with pytest.raises(ValueError):
+        kw.malloc_tune(0, 1 << 20)
+    with pytest.raises(ValueError):
+        kw.malloc_tune(64 << 20, 1 << 20)
