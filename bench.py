@@ -475,6 +475,20 @@ class Fixtures:
             shutil.rmtree(self.verify_dir, ignore_errors=True)
 
 
+async def fixture_tls_stats(fx) -> dict:
+    """The replay fixture's native TLS senders, summed over its workers:
+    cumulative ns sealing, waiting for queue room, and the writer threads
+    idle (waiting for sealed bytes: the fixture is the bound), in send(), and
+    waiting for the socket (the watcher is not reading: it is the bound)."""
+    reply = await fx.cmd("TLSSTATS")
+    tot: dict = {}
+    if reply and reply[0] == "TLS":
+        for w in json.loads(reply[1]):
+            for k, v in w.items():
+                tot[k] = tot.get(k, 0) + v
+    return tot
+
+
 async def reap_group(pgid: int, grace: float = 5.0) -> None:
     """Until no process of group ``pgid`` is left: SIGKILL after ``grace`` s."""
     deadline = time.monotonic() + grace
@@ -754,6 +768,7 @@ async def rank_main(args, d: Dist) -> dict:
         gc_stats = _GcStats()  # collector pauses on the loop thread over the timed steps
         hub = getattr(svc, "_reader_hub", None)
         hub0 = hub.stats() if hub is not None else None
+        fx_tls0 = await fixture_tls_stats(fx) if (args.api_tls and d.rank == 0) else None
         cpu0 = cpu_snapshot(fx)
         cg0 = cgroup_cpu()
         t0_mono = time.monotonic()  # the sink's stall times are CLOCK_MONOTONIC
@@ -783,7 +798,11 @@ async def rank_main(args, d: Dist) -> dict:
             dr, df, db = (hub1[k] - hub0[k] for k in ("recv_ns", "frame_ns", "recv_bytes"))
             reader_timed = {"recv_frac": round(dr / 1e9 / elapsed, 3), "frame_frac": round(df / 1e9 / elapsed, 3),
                             "recv_gb_per_s": round(db / dr, 2) if dr else None,
-                            "bytes_per_event": round(db / max(1, c["events_received"] - n0))}
+                            "bytes_per_event": round(db / max(1, c["events_received"] - n0)),
+                            # times a stream with bytes waited for a buffer: the pool short, the loop
+                            # still holding the stream's max_held, the byte budget spent
+                            "waits": {k: hub1.get(k, 0) - hub0.get(k, 0) for k in ("starved", "held_waits", "over_budget")},
+                            "reads": hub1["reads"] - hub0["reads"], "signals": hub1["signals"] - hub0["signals"]}
             if hub1.get("tls_taken") or hub1.get("tls_kept"):
                 # https: the reader thread's time opening records (its waits
                 # for the pool included) and each pool thread's busy share;
@@ -795,7 +814,16 @@ async def rank_main(args, d: Dist) -> dict:
                     "pooled_records": hub1["tls_pooled_records"] - hub0["tls_pooled_records"],
                     "pool_busy_frac": [round((a[0] - b[0]) / 1e9 / elapsed, 3)
                                        for a, b in zip(hub1["tls_pool"], hub0["tls_pool"])],
-                    "ct_gb_per_s": round((hub1["tls_ct_bytes"] - hub0["tls_ct_bytes"]) / 1e9 / elapsed, 2)}
+                    "ct_gb_per_s": round((hub1["tls_ct_bytes"] - hub0["tls_ct_bytes"]) / 1e9 / elapsed, 2),
+                    # the reader waiting for the pool after its own share, and in epoll_wait
+                    "ring_resizes": hub1.get("tls_ring_resizes", 0) - hub0.get("tls_ring_resizes", 0),
+                    "pool_wait_frac": round((hub1["tls_pool_wait_ns"] - hub0["tls_pool_wait_ns"]) / 1e9 / elapsed, 3),
+                    "reader_idle_frac": round((hub1["idle_ns"] - hub0["idle_ns"]) / 1e9 / elapsed, 3)}
+                if fx_tls0 is not None:  # the fixture's senders: which side waits for which
+                    fx_tls1 = await fixture_tls_stats(fx)
+                    reader_timed["tls"]["fixture"] = {
+                        k[:-3] + "_frac": round((fx_tls1.get(k, 0) - fx_tls0.get(k, 0)) / 1e9 / elapsed, 3)
+                        for k in ("seal_ns", "push_ns", "idle_ns", "send_ns", "pollout_ns")}
         zc = None
         if d.rank == 0:  # the replay fixture's zero-copy sends (bytes, slot waits) so far
             reply = await fx.cmd("ZCSTATS")

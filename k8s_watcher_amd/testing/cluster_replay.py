@@ -434,6 +434,7 @@ class Worker:
         self.sent_end: List[int] = []    # ... the resourceVersion of each range's last event (bisect)
         self.partial: Dict[int, int] = {}  # step -> g1 for steps sent only in part (they leave live pods)
         self.rv = RV0 - 1
+        self.tls_conns: set = set()  # live native TLS connections (TLSSTATS)
 
     # ------------------------------------------------------------------ state
     def scope(self, name: str) -> ScopeStream:
@@ -691,7 +692,11 @@ class Worker:
                 conn = await loop.run_in_executor(ex, tls.accept, fd)
             except OSError:
                 return
-            await self.handle(_TlsReader(conn), _TlsWriter(conn, ex))
+            self.tls_conns.add(conn)
+            try:
+                await self.handle(_TlsReader(conn), _TlsWriter(conn, ex))
+            finally:
+                self.tls_conns.discard(conn)
 
         while True:
             c, _ = await loop.sock_accept(self.sock)
@@ -733,6 +738,13 @@ class Worker:
             elif cmd == "ZCSTATS":  # zero-copy sends: bytes, slot waits
                 reply = json.dumps({n: {"bytes": r.bytes, "waits": r.waits} for n, r in self.rings.items()},
                                    separators=(",", ":"))
+            elif cmd == "TLSSTATS":  # native TLS sends: bytes and where the senders' time went (summed)
+                tot: Dict[str, int] = {"connections": 0}
+                for conn in list(self.tls_conns):
+                    tot["connections"] += 1
+                    for key, v in conn.stats().items():
+                        tot[key] = tot.get(key, 0) + v
+                reply = json.dumps(tot, separators=(",", ":"))
             out.write(reply.encode() + b"\n")
         if server is not None:
             server.close()
@@ -967,6 +979,8 @@ def run(args) -> None:
             print(f"SENT - {sum(int(r) for r in replies)}", flush=True)
         elif cmd == "ZCSTATS":
             print("ZC " + json.dumps([json.loads(r) for r in replies], separators=(",", ":")), flush=True)
+        elif cmd == "TLSSTATS":
+            print("TLS " + json.dumps([json.loads(r) for r in replies], separators=(",", ":")), flush=True)
         else:
             print("OK", flush=True)
     for pid, wr, _ in workers:

@@ -1,0 +1,18 @@
+# round 6: where one https cluster watch waits — the fixture's senders (sealing, waiting for the
+# socket) against the watcher's reader (recv, opening, epoll idle, buffer waits), plain http beside it.
+# usage: bash scripts/boxruns/tls_timeline.sh TAG [runs...]   (runs: tls plain tls64 plain64)
+set -o pipefail
+T=${1:-x}; shift
+O=gpurun_out/r6tt_$T
+mkdir -p $O
+B="python3 bench.py --steps 20 --warmup 5 --apart off --staging off --ref-events 0 --latency-seconds 5 --latency-seconds-high 5"
+i=0
+for r in "$@"; do
+  i=$((i+1))
+  case $r in
+    tls) X="--api-tls";; plain) X="";;
+    tls64) X="--api-tls --watch-scope discover --namespaces 64";; plain64) X="--watch-scope discover --namespaces 64";;
+    *) echo "unknown run $r"; exit 2;;
+  esac
+  timeout -k 10 300 $B $X --json-out $O/${i}_$r.json > $O/${i}_$r.out 2> $O/${i}_$r.err || exit $?
+done

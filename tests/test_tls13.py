@@ -516,7 +516,8 @@ def test_ring_memory_is_counted_in_the_pool_and_shrinks_with_the_class(pki):
     """The ciphertext ring is hub memory: it shows in ``allocated_bytes``
     (``watch_reader_allocated_bytes``) and ``tls_ring_bytes``, grows with the
     stream's buffer class and shrinks back when a quiet stream's class
-    drops (round-5 advisor)."""
+    drops (round-5 advisor) — after a second, not per read (a busy stream's
+    class moves between reads; a resize per read halved https throughput)."""
     burst = os.urandom(12_000_000)
     seen = {"max_ring": 0, "max_alloc": 0}
     srv = _listener()
@@ -529,7 +530,7 @@ def test_ring_memory_is_counted_in_the_pool_and_shrinks_with_the_class(pki):
         for _ in range(12):
             conn.send(b"q" * 500)
             conn.flush()
-            time.sleep(0.03)
+            time.sleep(0.15)  # quiet for 1.8 s: a ring shrinks after 1 s larger than needed
 
     t = threading.Thread(target=_serve, args=(pki, srv, script))
     t.start()
