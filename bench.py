@@ -824,6 +824,9 @@ async def rank_main(args, d: Dist) -> dict:
                     reader_timed["tls"]["fixture"] = {
                         k[:-3] + "_frac": round((fx_tls1.get(k, 0) - fx_tls0.get(k, 0)) / 1e9 / elapsed, 3)
                         for k in ("seal_ns", "push_ns", "idle_ns", "send_ns", "pollout_ns")}
+                    reader_timed["tls"]["fixture"]["sendfile_share"] = round(
+                        (fx_tls1.get("ring_bytes", 0) - fx_tls0.get("ring_bytes", 0))
+                        / max(1, hub1["tls_ct_bytes"] - hub0["tls_ct_bytes"]), 3)
         zc = None
         if d.rank == 0:  # the replay fixture's zero-copy sends (bytes, slot waits) so far
             reply = await fx.cmd("ZCSTATS")

@@ -780,6 +780,11 @@ class WatcherService:
             return
         loop_cpus, rest = split
         tids = list(self._decode_pool.thread_ids()) if self._decode_pool else []
+        # the hub's TLS pool threads (https watches) were made with the loop
+        # thread's whole domain: left there, three of them ran on the loop's
+        # core and it waited 5.8 ms/s for a CPU (profiles/r6/tls_timeline)
+        if self._reader_hub is not None:
+            tids += list(self._reader_hub.core.tls_thread_ids())
         reader_cpus = None
         reader_tid = self._reader_hub.core.thread_id() if self._reader_hub is not None else 0
         if reader_tid and mode == "auto":

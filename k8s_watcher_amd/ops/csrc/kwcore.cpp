@@ -33,6 +33,9 @@
 #include <netinet/tcp.h>
 #include <poll.h>
 #include <sys/epoll.h>
+#include <sys/ioctl.h>
+#include <sys/mman.h>
+#include <sys/sendfile.h>
 #include <sys/resource.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
@@ -44,6 +47,7 @@
 #include <algorithm>
 #include <array>
 #include <charconv>
+#include <chrono>
 #include <atomic>
 #include <cctype>
 #include <cerrno>

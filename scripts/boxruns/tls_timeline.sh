@@ -11,6 +11,7 @@ for r in "$@"; do
   i=$((i+1))
   case $r in
     tls) X="--api-tls";; plain) X="";;
+    tlsapart) X="--api-tls --fixture-placement apart";; plainapart) X="--fixture-placement apart";;
     tls64) X="--api-tls --watch-scope discover --namespaces 64";; plain64) X="--watch-scope discover --namespaces 64";;
     *) echo "unknown run $r"; exit 2;;
   esac
