@@ -103,20 +103,12 @@ def parse_args(argv=None):
     ap.add_argument("--assignment", default="balanced", choices=["balanced", "hash"])
     ap.add_argument("--profile", default="production", choices=["development", "staging", "production"])
     ap.add_argument("--engine", default="native", choices=["native", "python"])
-    ap.add_argument("--connections", type=int, default=None, help="notifier pool connections")
-    ap.add_argument("--pipeline-depth", type=int, default=None)
     ap.add_argument("--decode-threads", default=None, help="watcher.decode_threads (int or auto)")
-    ap.add_argument("--decode-affinity", default=None, choices=["auto", "none", "l3"])
-    ap.add_argument("--decode-spin-us", type=float, default=None,
-                    help="watcher.decode_spin_us: idle decode workers spin this long before sleeping")
-    ap.add_argument("--watch-read-bytes", type=int, default=None, help="watcher.watch_read_bytes")
-    ap.add_argument("--watch-reader", default=None, choices=["native", "asyncio"], help="watcher.watch_reader")
-    ap.add_argument("--watch-reader-buffers", type=int, default=None, help="watcher.watch_reader_buffers")
-    ap.add_argument("--watch-reader-max-bytes", type=int, default=None, help="watcher.watch_reader_max_bytes")
-    ap.add_argument("--reader-depth", type=int, default=None, help="watcher.watch_reader_depth (buffers per stream)")
-    ap.add_argument("--thread-pinning", default=None, choices=["auto", "loop", "none"], help="watcher.thread_pinning")
+    ap.add_argument("--set", dest="overrides", action="append", default=[], metavar="KEY=VALUE",
+                    help="override a watcher config key as main.py --set does (repeatable), e.g. "
+                         "clusterapi.pool.io_thread=on, watcher.watch_tls_threads=5, watcher.thread_pinning=none")
     ap.add_argument("--no-placement", dest="placement", action="store_false",
-                    help="no per-rank L3 domain assignment (each watcher still pins per watcher.decode_affinity)")
+                    help="no per-rank L3 domain assignment (each watcher's decode pool still keeps to one L3 domain)")
     ap.add_argument("--front-ends", default="per-rank", choices=["per-rank", "shared"],
                     help="per-rank: one API-server and one clusterapi front-end per rank, on its L3 domain "
                          "(one cluster behind them); shared: one of each for every rank, on rank 0's domain")
@@ -129,25 +121,8 @@ def parse_args(argv=None):
                     help="watcher.state_format (python_repr: the reference's str(V1ContainerState) text)")
     ap.add_argument("--validate", default=None, choices=["off", "payload", "full"],
                     help="watcher.validate (default payload: every raw token copied into a payload checked)")
-    ap.add_argument("--hub-dispatch", default=None, choices=["on", "off"],
-                    help="watcher.hub_dispatch: hub-read watches feed the native pipeline directly")
-    ap.add_argument("--partitioned-apply", default=None, choices=["on", "off"],
-                    help="watcher.partitioned_apply: a batch's apply split by pod-cache shard over the decode pool")
-    ap.add_argument("--hub-framing", default=None, choices=["auto", "on", "off"],
-                    help="watcher.hub_framing: the reader hub's thread de-chunks and splits bound watch bodies "
-                         "(auto: with several watch scopes)")
-    ap.add_argument("--python-pool", action="store_true", help="asyncio notifier pool instead of the C++ core")
-    ap.add_argument("--io-thread", action="store_true",
-                    help="serve the C++ notifier core's sockets on its own thread (clusterapi.pool.io_thread)")
-    ap.add_argument("--io-thread-auto", action="store_true", help="clusterapi.pool.io_thread: auto (the default)")
-    ap.add_argument("--io-thread-off", action="store_true",
-                    help="clusterapi.pool.io_thread: false (the event loop serves the notifier's sockets)")
     ap.add_argument("--tls", action="store_true",
                     help="https clusterapi (as production.yaml): the stub sink serves TLS with a throw-away CA")
-    ap.add_argument("--tls-records", default=None, choices=["native", "openssl"],
-                    help="watcher.watch_tls_records (https API server): the hub opens TLS 1.3 records itself, "
-                         "or SSL_read")
-    ap.add_argument("--tls-threads", type=int, default=None, help="watcher.watch_tls_threads (-1 auto)")
     ap.add_argument("--fixture-tls", default="native", choices=["native", "python"],
                     help="replay fixture's https: records sealed on a thread pool (native) or asyncio ssl")
     ap.add_argument("--fixture-tls-threads", type=int, default=3, help="sealing threads per fixture worker")
@@ -475,6 +450,26 @@ class Fixtures:
             shutil.rmtree(self.verify_dir, ignore_errors=True)
 
 
+def set_overrides(args) -> dict:
+    """--set KEY=VALUE expressions (repeatable) as one nested override dict,
+    applied over the bench's own (main.py --set's syntax: utils/config.py)."""
+    from k8s_watcher_amd.utils.config import deep_merge, parse_override
+    out: dict = {}
+    for expr in getattr(args, "overrides", None) or []:
+        out = deep_merge(out, parse_override(expr))
+    return out
+
+
+def set_value(args, key: str, default=None):
+    """The value --set gave the dotted ``key``, else ``default``."""
+    node = set_overrides(args)
+    for part in key.split("."):
+        if not isinstance(node, dict) or part not in node:
+            return default
+        node = node[part]
+    return node
+
+
 async def fixture_tls_stats(fx) -> dict:
     """The replay fixture's native TLS senders, summed over its workers:
     cumulative ns sealing, waiting for queue room, and the writer threads
@@ -528,7 +523,7 @@ async def rank_main(args, d: Dist) -> dict:
     from k8s_watcher_amd.kube.kubeconfig import KubeEndpoint
     from k8s_watcher_amd.metrics import Metrics
     from k8s_watcher_amd.testing.cluster_replay import namespace_names
-    from k8s_watcher_amd.utils.config import load_settings
+    from k8s_watcher_amd.utils.config import deep_merge, load_settings
     from k8s_watcher_amd.utils.logsetup import setup_logging
 
     scope = args.watch_scope if args.watch_scope != "auto" else ("cluster" if d.world == 1 else "discover")
@@ -549,13 +544,13 @@ async def rank_main(args, d: Dist) -> dict:
     if args.fixture_placement == "apart":
         # by default the fixtures run on the watchers' own L3 domains
         fx_cpus = fixture_cpus(all_cpus, held) if held else all_cpus
-    elif watcher_cpus and args.thread_pinning != "none":
+    elif watcher_cpus and set_value(args, "watcher.thread_pinning", "auto") != "none":
         # ... minus the physical cores watcher.thread_pinning gives the event-loop
         # thread (and, with auto, the reader thread)
         from k8s_watcher_amd.utils.cpus import loop_core_split, reader_core_split
         split = loop_core_split(watcher_cpus)
         fx_cpus = split[1] if split else None
-        if fx_cpus and args.thread_pinning in (None, "auto"):
+        if fx_cpus and set_value(args, "watcher.thread_pinning", "auto") == "auto":
             rsplit = reader_core_split(fx_cpus)
             fx_cpus = rsplit[1] if rsplit else fx_cpus
     elif watcher_cpus:
@@ -581,39 +576,10 @@ async def rank_main(args, d: Dist) -> dict:
                         "namespace_scope": "discover" if scope == "discover" else "client",
                         "shard": {"count": d.world, "index": d.rank, "assignment": args.assignment},
                         **({"decode_threads": args.decode_threads} if args.decode_threads is not None else {}),
-                        **({"decode_spin_us": args.decode_spin_us} if args.decode_spin_us is not None else {}),
-                        **({"watch_read_bytes": args.watch_read_bytes} if args.watch_read_bytes else {}),
-                        **({"watch_reader": args.watch_reader} if args.watch_reader else {}),
-                        **({"watch_reader_buffers": args.watch_reader_buffers} if args.watch_reader_buffers else {}),
-                        **({"watch_reader_max_bytes": args.watch_reader_max_bytes}
-                           if args.watch_reader_max_bytes is not None else {}),
-                        **({"watch_reader_depth": args.reader_depth} if args.reader_depth is not None else {}),
-                        **({"watch_tls_records": args.tls_records} if args.tls_records else {}),
-                        **({"watch_tls_threads": args.tls_threads} if args.tls_threads is not None else {}),
-                        **({"thread_pinning": args.thread_pinning} if args.thread_pinning else {}),
                         **({"validate": args.validate} if args.validate else {}),
-                        **({"hub_dispatch": args.hub_dispatch == "on"} if args.hub_dispatch else {}),
-                        **({"hub_framing": args.hub_framing} if args.hub_framing else {}),
-                        **({"partitioned_apply": args.partitioned_apply == "on"} if args.partitioned_apply else {}),
-                        **({"state_format": args.state_format} if args.state_format else {}),
-                        # placement already pinned this thread (the decode workers inherit it)
-                        **({"decode_affinity": args.decode_affinity or ("none" if watcher_cpus else "auto")})},
+                        **({"state_format": args.state_format} if args.state_format else {})},
         }
-        pool = {}
-        if args.connections:
-            pool["connections"] = args.connections
-        if args.pipeline_depth:
-            pool["pipeline_depth"] = args.pipeline_depth
-        if args.python_pool:
-            pool["native"] = False
-        if args.io_thread:
-            pool["io_thread"] = True
-        elif args.io_thread_auto:
-            pool["io_thread"] = "auto"
-        elif args.io_thread_off:
-            pool["io_thread"] = False
-        if pool:
-            overrides["clusterapi"]["pool"] = pool
+        overrides = deep_merge(overrides, set_overrides(args))
         settings = load_settings(args.profile, overrides=overrides)
         if settings.watcher.log_level:
             setup_logging(args.profile, settings.watcher.log_level, log_file=log_path)
@@ -1652,7 +1618,6 @@ def main(argv=None) -> int:
                             if d.world > 1 else f"single-process ({res['scope']} watch)"),
             "engine": args.engine,
             "validate": args.validate or "payload",
-            "partitioned_apply": args.partitioned_apply or "on",
             "state_format": args.state_format or "structured",
             "decode_threads": res["decode_threads"],
             "clusterapi": "https" if args.tls else "http",

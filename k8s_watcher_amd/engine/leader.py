@@ -294,7 +294,7 @@ class LeaderElector:
             delay = s.retry_period_seconds * (1.0 if self._leader else 1.0 + 0.2 * self.rng.random())
             if await self._sleep(delay):
                 break
-        if self._leader and s.release_on_shutdown:
+        if self._leader:  # hand the lease over at once (client-go ReleaseOnCancel)
             await self.release()
         self._set_leader(False)
 

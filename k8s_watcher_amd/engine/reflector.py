@@ -48,6 +48,12 @@ from .pipeline import EventPipeline
 # a watch that ends sooner than this without moving the resourceVersion is
 # treated like client-go's "very short watch": back off before reconnecting
 SHORT_WATCH_SECONDS = 1.0
+# native engine: a relist applies its LIST in slices of this much loop time
+# (the other scopes' watches and the notifier run between them)
+RELIST_SLICE_MS = 4.0
+# watch_list: an initial-events stream quiet this long without its
+# initial-events-end bookmark falls back to LIST
+WATCH_LIST_IDLE_SECONDS = 5.0
 
 class Expired(Exception):
     """The watch resourceVersion is too old (410 Gone)."""
@@ -170,7 +176,7 @@ class Reflector:
         """LIST + reconcile in the native engine (``ops/csrc/relist.inc``).
 
         Each page is applied as it arrives, in slices of at most
-        ``watcher.relist_slice_ms`` of loop time (the other scopes' watches and
+        ``RELIST_SLICE_MS`` of loop time (the other scopes' watches and
         the notifier run between them): decode, compare with the cache and
         notify happen in C++ with no Python object per pod. After the last page
         the scope's cached pods the LIST lacked are notified DELETED, also in
@@ -178,7 +184,7 @@ class Reflector:
         w = self.settings.watcher
         pipe = self.pipeline
         rl = pipe.native.relist(self.namespace if self._scoped() else None, notify)
-        budget_us = w.relist_slice_ms * 1000.0
+        budget_us = RELIST_SLICE_MS * 1000.0
         cont = None
         list_rv = None
         limit: Optional[int] = w.list_page_size
@@ -288,7 +294,7 @@ class Reflector:
 
         # native: the sink only cuts each read into segments (C++, no Python
         # object per pod) and queues them; the coroutine below applies them in
-        # watcher.relist_slice_ms slices with the loop free in between, and
+        # RELIST_SLICE_MS slices with the loop free in between, and
         # the socket stops being read while more than this is queued
         queue: list = []  # [(segments, read_ns)]
         queued = [0]
@@ -315,7 +321,7 @@ class Reflector:
                 self.stream._proto.set_reading(False)
 
         async def apply_queued() -> None:
-            budget_us = w.relist_slice_ms * 1000.0
+            budget_us = RELIST_SLICE_MS * 1000.0
             while queue and not end and not errors:
                 segs, read_ns = queue.pop(0)
                 for kind, payload in segs:
@@ -388,7 +394,7 @@ class Reflector:
             raise
         try:
             finished = self.stream.finished
-            idle = w.watch_list_idle_seconds
+            idle = WATCH_LIST_IDLE_SECONDS
             if wl is not None:
                 while not end and not errors and not self._stop.is_set():
                     if queue:
@@ -427,7 +433,7 @@ class Reflector:
         read_ns = time.monotonic_ns()
         if rl is not None:
             # the scope's cached pods the initial events did not contain: DELETED, in slices
-            budget_us = w.relist_slice_ms * 1000.0
+            budget_us = RELIST_SLICE_MS * 1000.0
             while True:
                 done, ctrl = pipe.native_slice(rl.sweep, budget_us, read_ns)
                 for ev in ctrl:
@@ -530,7 +536,7 @@ class Reflector:
             zero_copy=native is not None)  # the fused pipeline copies what it keeps (partial lines)
         self.watch_count += 1
         self.connected.set()
-        if (native is not None and framed[0] and w.hub_dispatch
+        if (native is not None and framed[0]
                 and self.stream.bind_native(native, on_native, pipeline.shared_flush(),
                                             (id(pipeline.notifier), id(pipeline.elog)),
                                             sync=pipeline.sync_native_log)):

@@ -51,6 +51,29 @@ from .pipeline import EventPipeline
 from .reflector import Reflector, WatchFailed
 
 
+# Fixed choices that were settings until round 6 (each one's A/B is in
+# BENCHMARKS.md; tests monkeypatch these module attributes):
+# the descriptor table grown once at start to hold this many fds (a watch per
+# namespace opens two each; growing it later, with threads running, waits an
+# RCU grace period per doubling: utils/fds.py)
+FD_TABLE_RESERVE = 16384
+# once every scope has synced, collect and freeze what start-up left
+# (gc.freeze): later full collections walk only objects made since, not the
+# service's long-lived ones (a 1,000-scope relist storm's gen-2 pauses);
+# unfrozen at shutdown. Start-up objects that later become cyclic garbage stay
+# until shutdown. Skipped when something is already frozen (an embedding
+# application's own freeze)
+GC_FREEZE = True
+# the reader hub's thread de-chunks and splits watch bodies (readerhub.inc
+# HubFramer): auto = with several watch scopes (namespace watches: the reader
+# has time, the loop has per-stream work), not for the one cluster-wide
+# watch, whose reader thread is the bound (profiles/r5/framing_ab,
+# r5/framing_many); on | off for tests
+HUB_FRAMING = "auto"
+MALLOC_TRIM_MIN_FREE = 16 << 20  # a periodic malloc_trim runs only when the C heap keeps this much free
+SPOOL_REPLAY_BATCH = 1000  # owed notifications re-submitted from the spool per replay pass
+
+
 class SetupError(Exception):
     """The Kubernetes client could not be set up (reference ``:246``)."""
 
@@ -231,12 +254,11 @@ class WatcherService:
     async def start(self) -> None:
         """Setup + start background tasks; returns once every scope has synced."""
         s = self.settings
-        if s.watcher.fd_table_reserve:
-            # before the decode pool, reader and I/O threads exist: growing a
-            # shared descriptor table later stalls the opening thread ~150 ms
-            # per doubling on a 256-CPU host (utils/fds.py)
-            from ..utils.fds import reserve_fd_table
-            reserve_fd_table(s.watcher.fd_table_reserve)
+        # before the decode pool, reader and I/O threads exist: growing a
+        # shared descriptor table later stalls the opening thread ~150 ms
+        # per doubling on a 256-CPU host (utils/fds.py)
+        from ..utils.fds import reserve_fd_table
+        reserve_fd_table(FD_TABLE_RESERVE)
         if self._native_pipeline() and s.watcher.malloc_trim_seconds > 0:
             # fixed glibc thresholds before the cache and the buffers exist:
             # blocks >= 512 KiB on their own mappings (unmapped when freed),
@@ -244,7 +266,7 @@ class WatcherService:
             # soak: RSS grew with retained free bytes; kwcore.cpp malloc_tune)
             from ..ops.native import load as _load_kw
             _load_kw().malloc_tune(512 << 10, 4 << 20)
-        if s.watcher.gc_freeze and gc.get_freeze_count() == 0:
+        if GC_FREEZE and gc.get_freeze_count() == 0:
             # what import and configuration made is permanent: the full
             # collections that starting a thousand scopes triggers then walk
             # only the scopes' own objects (70-140 ms gen-2 pauses otherwise).
@@ -275,7 +297,7 @@ class WatcherService:
             if len(self.spool):
                 self.log.warning(f"Spool {sp.path} holds {len(self.spool)} notifications from an earlier run")
             self.spool_replayer = SpoolReplayer(self.spool, self.notifier, self.metrics,
-                                                sp.replay_interval_seconds, sp.replay_batch)
+                                                sp.replay_interval_seconds, SPOOL_REPLAY_BATCH)
             self._tasks.append(asyncio.ensure_future(self.spool_replayer.run()))
         self.decoder = make_decoder(s.watcher.engine, s.environment, s.watcher.state_format,
                                     s.watcher.payload_extra, s.watcher.validate)
@@ -318,7 +340,7 @@ class WatcherService:
         if self._native_pipeline():
             from ..ops.native import load as _load_native
             _kw = _load_native()
-            _kw.set_partitioned_apply(s.watcher.partitioned_apply)
+            _kw.set_partitioned_apply(True)
             # which apply path ran, and how much of it (cumulative, process-wide)
             for _key in ("partitioned_batches", "partitioned_lines", "tail_serial_lines", "tail_submits",
                          "tail_lock_runs", "serial_batches", "serial_lines"):
@@ -334,9 +356,8 @@ class WatcherService:
                 self._reader_hub = WatchReaderHub(s.watcher.watch_read_bytes or (4 << 20),
                                                   s.watcher.watch_reader_buffers,
                                                   max_bytes=s.watcher.watch_reader_max_bytes,
-                                                  frame=(s.watcher.hub_framing == "on" or
-                                                         (s.watcher.hub_framing == "auto" and self._multi)),
-                                                  depth=s.watcher.watch_reader_depth,
+                                                  frame=(HUB_FRAMING == "on" or
+                                                         (HUB_FRAMING == "auto" and self._multi)),
                                                   tls_records=s.watcher.watch_tls_records == "native",
                                                   tls_threads=(s.watcher.watch_tls_threads
                                                                if s.watcher.watch_tls_threads >= 0
@@ -749,16 +770,16 @@ class WatcherService:
         from ..utils.cpus import auto_decode_spin_us, auto_decode_threads, pin_to_l3_domain
         w = self.settings.watcher
         n = w.decode_threads if w.decode_threads >= 0 else auto_decode_threads()
-        if n > 0 and w.decode_affinity != "none":
+        if n > 0:
             # Workers started below inherit the mask. Measured on a chiplet
             # host (BENCHMARKS.md): 3 workers spread over CCDs were slower than
             # none; the same 3 inside the loop thread's L3 ran ~1.6x faster.
-            auto = w.decode_affinity == "auto"
-            dom = pin_to_l3_domain(min_cpus=n + 1 if auto else 1, only_if_split=auto,
-                                   index=w.decode_l3_domain)
+            # A process already inside one L3 domain (a launcher placed it)
+            # stays where it is.
+            dom = pin_to_l3_domain(min_cpus=n + 1, only_if_split=True)
             if dom:
                 self.log.info(f"Decode pool pinned to L3 domain CPUs {sorted(dom)}")
-        spin = w.decode_spin_us if w.decode_spin_us >= 0 else auto_decode_spin_us()
+        spin = auto_decode_spin_us()
         return load().DecodePool(n, spin) if n > 0 else 0
 
     def _pin_threads(self) -> None:
@@ -1027,7 +1048,7 @@ class WatcherService:
 
         A trim locks each arena while it walks it, and a thread allocating
         from that arena waits: it runs only when the heap retains at least
-        ``watcher.malloc_trim_min_free_mb`` free, and every trim is timed
+        ``MALLOC_TRIM_MIN_FREE`` free, and every trim is timed
         (``malloc_trim_last_ms`` / ``malloc_trim_max_ms`` gauges,
         ``malloc_trim_us`` counter) so a latency outlier can be checked
         against it. It waits for half a second
@@ -1036,7 +1057,7 @@ class WatcherService:
         from ..ops.native import load
         kw = load()
         trim, info = kw.malloc_trim, kw.malloc_info
-        min_free = self.settings.watcher.malloc_trim_min_free_mb * (1 << 20)
+        min_free = MALLOC_TRIM_MIN_FREE
         loop = asyncio.get_running_loop()
         c, g = self.metrics.c, self.metrics.gauges
         last = {"last_ms": 0.0, "max_ms": 0.0}

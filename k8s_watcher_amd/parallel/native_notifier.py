@@ -44,6 +44,12 @@ from .notifier import RETRYABLE_STATUS
 
 
 class NativeNotifierPool:
+    # io_thread: auto — notifications/s above which the I/O thread takes the
+    # sockets, below which they come back to the loop (measured:
+    # profiles/io_thread_auto_gpu_box.md)
+    IO_THREAD_ON_RATE = 50000.0
+    IO_THREAD_OFF_RATE = 5000.0
+
     def __init__(self, settings: ClusterApiSettings, metrics: Optional[Metrics] = None,
                  ts_mode: str = "local", log_events: bool = False,
                  on_saturation: Optional[Callable[[bool], None]] = None,
@@ -104,7 +110,7 @@ class NativeNotifierPool:
         self.spool = None
         # clusterapi.pool.io_thread: the core serves the sockets on its own
         # thread (epoll) and signals this eventfd when Python has work to do
-        self.threaded = settings.pool.io_thread
+        self.threaded = settings.pool.io_thread == "on"
         self._py_fd = -1
         if self.threaded:
             self._py_fd = self.core.start_io()
@@ -112,12 +118,12 @@ class NativeNotifierPool:
         self._watchdog = self.loop.create_task(self._watchdog_loop())
         # io_thread: auto — the loop serves the sockets while notifications are
         # few (lowest latency: no cross-thread hand-off per request); above
-        # io_thread_on_rate the I/O thread takes them (the loop keeps its time
-        # for decoding and applying events), below io_thread_off_rate they
+        # IO_THREAD_ON_RATE the I/O thread takes them (the loop keeps its time
+        # for decoding and applying events), below IO_THREAD_OFF_RATE they
         # come back (requests still in flight are answered on the loop). Sampled
         # every 100 ms; switching needs two samples in a row.
         self._auto = None
-        if settings.pool.io_thread_auto:
+        if settings.pool.io_thread == "auto":
             self._auto = self.loop.create_task(self._auto_io_loop())
 
     # ------------------------------------------------------------------ spool (parallel/spool.py)
@@ -315,7 +321,7 @@ class NativeNotifierPool:
         self._after()  # writers for unsent bytes, counters
 
     async def _auto_io_loop(self) -> None:
-        on, off = self.settings.pool.io_thread_on_rate, self.settings.pool.io_thread_off_rate
+        on, off = self.IO_THREAD_ON_RATE, self.IO_THREAD_OFF_RATE
         period = 0.1
         c = self.metrics.c
         last = c["notify_submitted"]

@@ -174,10 +174,10 @@ def _as_int(value: Any, key: str) -> int:
     return out
 
 
-def _hub_framing(value: Any) -> str:
+def _io_thread(value: Any) -> str:
     if value == "auto":
         return "auto"
-    return "on" if _as_bool(value, "watcher.hub_framing") else "off"
+    return "on" if _as_bool(value, "clusterapi.pool.io_thread") else "off"
 
 
 def _bounded_int(value: Any, key: str, lo: int, hi: int) -> int:
@@ -187,11 +187,30 @@ def _bounded_int(value: Any, key: str, lo: int, hi: int) -> int:
     return n
 
 
-def _reader_depth(value: Any) -> int:
-    n = _as_int(value, "watcher.watch_reader_depth")
-    if not 2 <= n <= 8:
-        raise ConfigError(f"watcher.watch_reader_depth: 2..8 buffers, got {n}")
-    return n
+# Keys that were settings once and are fixed now (their A/B measured, the
+# winner kept: BENCHMARKS.md "Settings retired in round 6"). A config that
+# still sets one loads; the value is ignored with a warning. watch_interval
+# is the reference's key (a watch never polls): accepted silently.
+RETIRED_KEYS = {
+    "watcher": ("watch_list_idle_seconds", "watch_reader_depth", "hub_dispatch", "hub_framing",
+                "partitioned_apply", "relist_slice_ms", "decode_affinity", "decode_l3_domain",
+                "decode_spin_us", "malloc_trim_min_free_mb", "gc_freeze", "fd_table_reserve"),
+    "clusterapi.pool": ("io_thread_on_rate", "io_thread_off_rate"),
+    "clusterapi.spool": ("replay_batch",),
+    "watcher.leader_election": ("release_on_shutdown",),
+}
+
+
+def retired_keys_in(cfg: Dict[str, Any]) -> List[str]:
+    """The retired keys a merged config still sets (dotted paths)."""
+    found = []
+    for section, keys in RETIRED_KEYS.items():
+        node: Any = cfg
+        for part in section.split("."):
+            node = node.get(part) if isinstance(node, dict) else None
+        if isinstance(node, dict):
+            found += [f"{section}.{k}" for k in keys if k in node]
+    return found
 
 
 def _choice(value: Any, key: str, choices: tuple) -> str:
@@ -240,10 +259,11 @@ class NotifierPoolSettings:
     max_queued_bytes: int = 64 << 20  # backpressure also past this many owed body bytes
     coalesce: bool = False
     native: bool = True  # C++ notifier core (watcher.engine: native)
-    io_thread: bool = False  # native core serves its sockets on a dedicated thread (profiles/notifier_io_thread_gpu_box.md)
-    io_thread_auto: bool = False  # io_thread: auto — on while notifications run above io_thread_on_rate
-    io_thread_on_rate: float = 50000.0  # notifications/s (auto): hand the sockets to the I/O thread
-    io_thread_off_rate: float = 5000.0  # notifications/s (auto): back to the event loop (low latency)
+    # on: the native core serves its sockets on a dedicated thread
+    # (profiles/notifier_io_thread_gpu_box.md); off: the event loop does;
+    # auto: the thread while notifications run fast (parallel/native_notifier.py);
+    # the config files' default is auto
+    io_thread: str = "off"
 
 
 @dataclass
@@ -255,7 +275,6 @@ class SpoolSettings:
     segment_bytes: int = 64 << 20
     fsync: bool = False
     replay_interval_seconds: float = 5.0
-    replay_batch: int = 1000
 
 
 @dataclass
@@ -304,7 +323,6 @@ class LeaderElectionSettings:
     lease_duration_seconds: float = 15.0
     renew_deadline_seconds: float = 10.0
     retry_period_seconds: float = 2.0
-    release_on_shutdown: bool = True
     exit_on_loss: bool = False
 
 
@@ -321,38 +339,23 @@ class WatcherSettings:
     notify_on: str = "all"  # all | phase_change
     initial_list: str = "notify"  # notify | skip
     initial_sync: str = "list"  # list | watch_list (sendInitialEvents, LIST fallback)
-    watch_list_idle_seconds: float = 5.0
     payload_extra: int = 0  # watcher.payload_extra_fields as a models.payload.extra_mask
     watch_read_bytes: int = 4 << 20  # bytes per socket read on a plain-TCP watch (asyncio default 256 KiB)
     watch_reader: str = "native"  # native (ReaderHub thread, plain TCP + native engine) | asyncio
     watch_reader_buffers: int = 64  # ReaderHub pool: up to this many buffers of watch_read_bytes (allocated on use)
     watch_reader_max_bytes: int = 0  # ReaderHub read-ahead over all streams (0: the whole pool)
-    watch_reader_depth: int = 2  # ReaderHub read-ahead per stream, in buffers (2..8)
     # https watches: the reader hub reads and opens TLS 1.3 records itself
     # (native; openssl: SSL_read on the reader thread), on this many pool
     # threads besides the reader thread (-1: auto, utils/cpus.py)
     watch_tls_records: str = "native"
     watch_tls_threads: int = -1
-    hub_dispatch: bool = True  # hub-read watches feed the native pipeline with no Python call per read
-    # ... and the hub's thread de-chunks and splits their bodies (readerhub.inc
-    # HubFramer): auto = with several watch scopes (namespace watches: the
-    # reader has time, the loop has per-stream work), not for the one
-    # cluster-wide watch, whose reader thread is the bound (it then only
-    # receives; the loop frames: profiles/r5/framing_ab, r5/framing_many)
-    hub_framing: str = "auto"  # auto | on | off
-    partitioned_apply: bool = True  # a batch's apply split by pod-cache shard over the decode pool (engine.inc)
     thread_pinning: str = "auto"  # auto: loop thread and reader thread on cores of their own in one L3 | loop | none
     retry: RetryPolicy = field(default_factory=lambda: RetryPolicy(3, 5.0))
     watch_timeout_seconds: int = 300
     list_page_size: int = 500
-    relist_slice_ms: float = 4.0  # native engine: a relist applies its LIST in slices of this much loop time
     relist_concurrency: int = 16  # scopes LISTing at once (a compaction 410s every namespace watch together); 0 = no cap
-    watch_interval: float = 1.0  # accepted for schema parity; a watch has no poll interval
     engine: str = "native"  # native | python
     decode_threads: int = -1  # native engine: extra watch-decode threads, -1 = auto (utils/cpus.py)
-    decode_affinity: str = "auto"  # auto | l3 | none: keep loop thread + decode workers in one L3 domain
-    decode_l3_domain: int = -1  # with affinity: index into the host's L3 domains, -1 = the current one
-    decode_spin_us: float = -1.0  # idle decode worker spins this long before it sleeps (0 = at once, -1 = auto)
     state_format: str = "structured"  # structured | python_repr
     # native engine: payload (every raw JSON token copied into a payload passes json.loads' rules) |
     # full (each whole watch line and LIST item must: INVALID exactly when the Python engine's json.loads
@@ -364,20 +367,6 @@ class WatcherSettings:
     # native engine: every this many seconds the C heap's free pages go back to
     # the kernel (malloc_trim, off the event loop); 0 = never
     malloc_trim_seconds: float = 60.0
-    malloc_trim_min_free_mb: float = 16.0  # ... only when the C heap holds at least this much free (retained) memory
-    # once every scope has synced, collect and freeze what start-up left
-    # (gc.freeze): later full collections then walk only objects made since,
-    # not the service's long-lived ones (a 1,000-scope relist storm's gen-2
-    # pauses); unfrozen again at shutdown. The cost is bounded and one-time:
-    # start-up objects that later become cyclic garbage (a namespace's
-    # reflector stopped in discover mode, the first watch connections'
-    # transport cycles) stay until shutdown, they are never re-frozen. Skipped
-    # when something is already frozen (an embedding application's own freeze)
-    gc_freeze: bool = True
-    # the descriptor table grown once at start to hold this many fds (a watch
-    # per namespace opens two each; growing it later, with threads running,
-    # waits an RCU grace period per doubling: utils/fds.py); 0 = as needed
-    fd_table_reserve: int = 16384
     shard: "ShardSettings" = field(default_factory=lambda: ShardSettings())
     leader_election: LeaderElectionSettings = field(default_factory=LeaderElectionSettings)
 
@@ -461,9 +450,8 @@ def _spool(block: Dict[str, Any]) -> SpoolSettings:
         segment_bytes=_as_int(block.get("segment_bytes", 64 << 20), f"{key}.segment_bytes"),
         fsync=_as_bool(block.get("fsync", False), f"{key}.fsync"),
         replay_interval_seconds=_as_float(block.get("replay_interval_seconds", 5), f"{key}.replay_interval_seconds"),
-        replay_batch=_as_int(block.get("replay_batch", 1000), f"{key}.replay_batch"),
     )
-    if sp.max_bytes <= 0 or sp.segment_bytes <= 0 or sp.replay_batch <= 0 or sp.replay_interval_seconds <= 0:
+    if sp.max_bytes <= 0 or sp.segment_bytes <= 0 or sp.replay_interval_seconds <= 0:
         raise ConfigError(f"{key}: sizes, batch and interval must be positive")
     return sp
 
@@ -478,7 +466,6 @@ def _leader_election(block: Dict[str, Any]) -> LeaderElectionSettings:
         lease_duration_seconds=_as_float(block.get("lease_duration_seconds", 15), f"{key}.lease_duration_seconds"),
         renew_deadline_seconds=_as_float(block.get("renew_deadline_seconds", 10), f"{key}.renew_deadline_seconds"),
         retry_period_seconds=_as_float(block.get("retry_period_seconds", 2), f"{key}.retry_period_seconds"),
-        release_on_shutdown=_as_bool(block.get("release_on_shutdown", True), f"{key}.release_on_shutdown"),
         exit_on_loss=_as_bool(block.get("exit_on_loss", False), f"{key}.exit_on_loss"),
     )
     if not 0 < le.retry_period_seconds < le.renew_deadline_seconds < le.lease_duration_seconds:
@@ -499,6 +486,9 @@ def _decode_threads(v: Any) -> int:
 
 def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
     """Validate the merged dict into :class:`Settings` (raises :class:`ConfigError`)."""
+    for key in retired_keys_in(cfg):
+        logging.getLogger("k8s_watcher_amd.config").warning(
+            f"Config key {key} is no longer a setting (fixed; see docs/OPERATIONS.md): ignored")
     k = cfg.get("kubernetes") or {}
     w = cfg.get("watcher") or {}
     c = cfg.get("clusterapi") or {}
@@ -537,38 +527,23 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
         notify_on=_choice(w.get("notify_on", "all"), "watcher.notify_on", ("all", "phase_change")),
         initial_list=_choice(w.get("initial_list", "notify"), "watcher.initial_list", ("notify", "skip")),
         initial_sync=_choice(w.get("initial_sync", "list"), "watcher.initial_sync", ("list", "watch_list")),
-        watch_list_idle_seconds=_as_float(w.get("watch_list_idle_seconds", 5), "watcher.watch_list_idle_seconds"),
         payload_extra=_payload_extra(w.get("payload_extra_fields") or []),
         watch_read_bytes=max(0, _as_int(w.get("watch_read_bytes", 4 << 20), "watcher.watch_read_bytes")),
         watch_reader=_choice(w.get("watch_reader", "native"), "watcher.watch_reader", ("native", "asyncio")),
         watch_reader_buffers=max(2, _as_int(w.get("watch_reader_buffers", 64), "watcher.watch_reader_buffers")),
         watch_reader_max_bytes=max(0, _as_int(w.get("watch_reader_max_bytes", 0), "watcher.watch_reader_max_bytes")),
-        watch_reader_depth=_reader_depth(w.get("watch_reader_depth", 2)),
         watch_tls_records=_choice(w.get("watch_tls_records", "native"), "watcher.watch_tls_records",
                                   ("native", "openssl")),
         watch_tls_threads=_bounded_int(w.get("watch_tls_threads", -1), "watcher.watch_tls_threads", -1, 32),
-        hub_dispatch=_as_bool(w.get("hub_dispatch", True), "watcher.hub_dispatch"),
-        hub_framing=_hub_framing(w.get("hub_framing", "auto")),
-        partitioned_apply=_as_bool(w.get("partitioned_apply", True), "watcher.partitioned_apply"),
         malloc_trim_seconds=_bounded_float(w.get("malloc_trim_seconds", 60.0), "watcher.malloc_trim_seconds",
                                            0.0, 86400.0),
-        malloc_trim_min_free_mb=_bounded_float(w.get("malloc_trim_min_free_mb", 16.0), "watcher.malloc_trim_min_free_mb",
-                                               0.0, 1e6),
-        gc_freeze=_as_bool(w.get("gc_freeze", True), "watcher.gc_freeze"),
-        fd_table_reserve=max(0, _as_int(w.get("fd_table_reserve", 16384), "watcher.fd_table_reserve")),
         thread_pinning=_choice(w.get("thread_pinning", "auto"), "watcher.thread_pinning", ("auto", "loop", "none")),
         retry=_retry(w.get("retry"), "watcher.retry", RetryPolicy(3, 5.0), min_attempts=0),
         watch_timeout_seconds=_as_int(w.get("watch_timeout_seconds", 300), "watcher.watch_timeout_seconds"),
         list_page_size=max(1, _as_int(w.get("list_page_size", 500), "watcher.list_page_size")),
-        relist_slice_ms=_bounded_float(w.get("relist_slice_ms", 4), "watcher.relist_slice_ms", 0.1, 10000.0),
         relist_concurrency=max(0, _as_int(w.get("relist_concurrency", 16), "watcher.relist_concurrency")),
-        watch_interval=_as_float(w.get("watch_interval", 1), "watcher.watch_interval"),
         engine=_choice(w.get("engine", "native"), "watcher.engine", ("native", "python")),
         decode_threads=_decode_threads(w.get("decode_threads", "auto")),
-        decode_affinity=_choice(w.get("decode_affinity", "auto"), "watcher.decode_affinity", ("auto", "l3", "none")),
-        decode_l3_domain=_as_int(w.get("decode_l3_domain", -1), "watcher.decode_l3_domain"),
-        decode_spin_us=(-1.0 if str(w.get("decode_spin_us", "auto")).strip().lower() == "auto"
-                        else _bounded_float(w.get("decode_spin_us"), "watcher.decode_spin_us", 0.0, 1e6)),
         state_format=_choice(w.get("state_format", "structured"), "watcher.state_format", ("structured", "python_repr")),
         validate=_choice(w.get("validate", "payload"), "watcher.validate", ("off", "payload", "full")),
         event_timestamp=_choice(w.get("event_timestamp", "local"), "watcher.event_timestamp", ("local", "utc")),
@@ -600,13 +575,7 @@ def settings_from_dict(environment: str, cfg: Dict[str, Any]) -> Settings:
                                                   "clusterapi.pool.max_queued_bytes")),
             coalesce=_as_bool(pool.get("coalesce", False), "clusterapi.pool.coalesce"),
             native=_as_bool(pool.get("native", True), "clusterapi.pool.native"),
-            io_thread=(pool.get("io_thread", "auto") != "auto"
-                       and _as_bool(pool.get("io_thread", False), "clusterapi.pool.io_thread")),
-            io_thread_auto=pool.get("io_thread", "auto") == "auto",
-            io_thread_on_rate=_bounded_float(pool.get("io_thread_on_rate", 50000), "clusterapi.pool.io_thread_on_rate",
-                                             1.0, 1e9),
-            io_thread_off_rate=_bounded_float(pool.get("io_thread_off_rate", 5000),
-                                              "clusterapi.pool.io_thread_off_rate", 0.0, 1e9),
+            io_thread=_io_thread(pool.get("io_thread", "auto")),
         ),
         verify_tls=_as_bool(c.get("verify_tls", True), "clusterapi.verify_tls"),
         ca_file=c.get("ca_file") or None,

@@ -126,3 +126,25 @@ def test_retry_policy_delays():
     r = s.watcher.retry
     assert [r.delay(i) for i in (1, 2, 3)] == [5, 10, 20]
     assert r.delay(100) == r.max_delay_seconds
+
+
+def test_retired_keys_load_with_a_warning(caplog):
+    """Settings retired in round 6 (fixed at their measured winner) still load
+    from an operator's file: ignored, each named in a warning; the reference's
+    watch_interval is accepted silently."""
+    import logging
+
+    from k8s_watcher_amd.utils.config import load_settings, retired_keys_in
+    ov = {"watcher": {"hub_framing": "on", "gc_freeze": False, "watch_interval": 3,
+                      "leader_election": {"release_on_shutdown": False}},
+          "clusterapi": {"pool": {"io_thread_on_rate": 10}, "spool": {"replay_batch": 5}}}
+    with caplog.at_level(logging.WARNING, logger="k8s_watcher_amd.config"):
+        s = load_settings("production", overrides=ov, environ={})
+    named = sorted(retired_keys_in(s.raw))
+    assert named == ["clusterapi.pool.io_thread_on_rate", "clusterapi.spool.replay_batch", "watcher.gc_freeze",
+                     "watcher.hub_framing", "watcher.leader_election.release_on_shutdown"]
+    text = caplog.text
+    assert all(k in text for k in named) and "watch_interval" not in text
+    assert s.clusterapi.pool.io_thread == "auto"
+    assert load_settings("production", overrides={"clusterapi": {"pool": {"io_thread": True}}},
+                         environ={}).clusterapi.pool.io_thread == "on"

@@ -140,14 +140,16 @@ def test_lifecycle_order_per_pod():
 
 
 @pytest.mark.parametrize("freeze", [True, False])
-def test_gc_freeze_after_sync_and_unfreeze_at_shutdown(freeze):
-    """watcher.gc_freeze: start-up's survivors are frozen once every scope has
+def test_gc_freeze_after_sync_and_unfreeze_at_shutdown(freeze, monkeypatch):
+    """service.GC_FREEZE: start-up's survivors are frozen once every scope has
     synced (full collections skip them), and unfrozen at shutdown so a retired
     service (a leader's last term) is collectable."""
     import gc
 
     async def body():
-        srv, sink, svc = await start_stack(overrides={"watcher": {"gc_freeze": freeze}})
+        from k8s_watcher_amd.engine import service
+        monkeypatch.setattr(service, "GC_FREEZE", freeze)
+        srv, sink, svc = await start_stack()
         base = gc.get_freeze_count()
         await svc.start()
         during = gc.get_freeze_count()
@@ -170,7 +172,7 @@ def test_gc_freeze_leaves_an_embedders_freeze_alone():
     import gc
 
     async def body():
-        srv, sink, svc = await start_stack(overrides={"watcher": {"gc_freeze": True}})
+        srv, sink, svc = await start_stack()
         gc.freeze()
         mine = gc.get_freeze_count()
         try:
@@ -190,12 +192,14 @@ def test_gc_freeze_leaves_an_embedders_freeze_alone():
 
 @pytest.mark.parametrize("scope,framing,want", [("client", "auto", False), ("discover", "auto", True),
                                                 ("client", "on", True), ("discover", "off", False)])
-def test_hub_framing_auto_follows_the_watch_shape(scope, framing, want):
-    """watcher.hub_framing: auto — the reader thread frames bodies when there
+def test_hub_framing_auto_follows_the_watch_shape(scope, framing, want, monkeypatch):
+    """service.HUB_FRAMING: auto — the reader thread frames bodies when there
     are several watch scopes, and leaves the one cluster-wide watch's framing
     to the loop (that reader thread is the bound: profiles/r5/framing_ab)."""
     async def body():
-        srv, sink, svc = await start_stack(overrides={"watcher": {"namespace_scope": scope, "hub_framing": framing}})
+        from k8s_watcher_amd.engine import service
+        monkeypatch.setattr(service, "HUB_FRAMING", framing)
+        srv, sink, svc = await start_stack(overrides={"watcher": {"namespace_scope": scope}})
         await svc.start()
         got = svc._reader_hub.frame
         svc.stop()

@@ -132,7 +132,7 @@ def test_round4_paths_on_host():
     line = run_bench(["--steps", "3", "--warmup", "1",
                           "--rounds-per-step", "4", "--apart", "off", "--staging", "off", "--ref-events", "0",
                           "--latency-seconds", "0", "--latency-seconds-high", "2", "--probe"])
-    assert line["verify"]["exactly_once"] and line["config"]["partitioned_apply"] == "on"
+    assert line["verify"]["exactly_once"]
     assert line["loop_probe_rank0"]["partitioned_batches"] > 0
     assert sum(s.get("*", {}).get("bytes", 0) for s in line["fixture_zero_copy"]) > 0
     assert line["latency_high_seconds_rank0"]["rows"] and "rate_dips_rank0" in line

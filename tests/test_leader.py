@@ -312,7 +312,7 @@ def test_terms_do_not_leak_decode_pool_threads():
         sink = StubSink()
         await sink.start()
         ov = {"clusterapi": {"base_url": sink.url, "retry": {"delay_seconds": 0.01}},
-              "watcher": {"engine": "native", "decode_threads": 3, "decode_affinity": "none",
+              "watcher": {"engine": "native", "decode_threads": 3,
                           "retry": {"delay_seconds": 0.01, "max_attempts": 0},
                           "leader_election": {"enabled": True, "identity": "solo", "exit_on_loss": False,
                                               **FAST}}}

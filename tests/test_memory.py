@@ -32,21 +32,21 @@ def test_malloc_trim_setting():
         load_settings("production", overrides={"watcher": {"malloc_trim_seconds": -1}}, environ={})
 
 
-def _trim_stub(min_free_mb):
+def _trim_stub(min_free_mb, monkeypatch):
     import types
 
+    from k8s_watcher_amd.engine import service
     from k8s_watcher_amd.metrics import Metrics
-    return types.SimpleNamespace(metrics=Metrics(), log=__import__("logging").getLogger("test"),
-                                 settings=types.SimpleNamespace(watcher=types.SimpleNamespace(
-                                     malloc_trim_min_free_mb=min_free_mb)))
+    monkeypatch.setattr(service, "MALLOC_TRIM_MIN_FREE", int(min_free_mb * (1 << 20)))
+    return types.SimpleNamespace(metrics=Metrics(), log=__import__("logging").getLogger("test"))
 
 
-def test_service_trims_periodically():
+def test_service_trims_periodically(monkeypatch):
     """The service's trim loop runs the trim off the event loop, counts and times it."""
     from k8s_watcher_amd.engine.service import WatcherService
 
     async def body():
-        stub = _trim_stub(0.0)
+        stub = _trim_stub(0.0, monkeypatch)
         task = asyncio.ensure_future(WatcherService._malloc_trim_loop(stub, 0.01))
         await asyncio.sleep(1.4)  # each trim waits for a quiet half second first
         task.cancel()
@@ -57,13 +57,13 @@ def test_service_trims_periodically():
     assert m.c["malloc_trim_us"] > 0 and m.gauges["malloc_trim_max_ms"]() >= m.gauges["malloc_trim_last_ms"]() > 0
 
 
-def test_service_skips_trim_below_free_threshold():
-    """watcher.malloc_trim_min_free_mb: no trim (no arena walk under their
+def test_service_skips_trim_below_free_threshold(monkeypatch):
+    """service.MALLOC_TRIM_MIN_FREE: no trim (no arena walk under their
     locks) while the heap retains less free memory than that."""
     from k8s_watcher_amd.engine.service import WatcherService
 
     async def body():
-        stub = _trim_stub(1e6)  # a terabyte: never reached
+        stub = _trim_stub(1e6, monkeypatch)  # a terabyte: never reached
         task = asyncio.ensure_future(WatcherService._malloc_trim_loop(stub, 0.01))
         await asyncio.sleep(0.15)
         task.cancel()
@@ -73,13 +73,13 @@ def test_service_skips_trim_below_free_threshold():
     assert m.c.get("malloc_trims", 0) == 0 and m.c["malloc_trims_skipped"] >= 2
 
 
-def test_service_defers_trim_under_load():
+def test_service_defers_trim_under_load(monkeypatch):
     """Under sustained traffic the trim waits for a quiet moment (the freed
     pages would be reused at once, and a trim stalls allocating threads)."""
     from k8s_watcher_amd.engine.service import WatcherService
 
     async def body():
-        stub = _trim_stub(0.0)
+        stub = _trim_stub(0.0, monkeypatch)
         task = asyncio.ensure_future(WatcherService._malloc_trim_loop(stub, 0.05))
         t_end = asyncio.get_running_loop().time() + 1.2
         while asyncio.get_running_loop().time() < t_end:  # ~20k events/s

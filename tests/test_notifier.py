@@ -35,7 +35,7 @@ def core(uid, phase="Running", name=None):
 def _threaded_native(s, metrics=None, **kw):
     """The native core serving its sockets on its own thread (``clusterapi.pool.io_thread``)."""
     import dataclasses
-    return NativeNotifierPool(dataclasses.replace(s, pool=dataclasses.replace(s.pool, io_thread=True)),
+    return NativeNotifierPool(dataclasses.replace(s, pool=dataclasses.replace(s.pool, io_thread="on")),
                               metrics, **kw)
 
 
@@ -405,19 +405,20 @@ def test_compat_clients_honour_retry_after():
     assert t_async >= 0.18 and t_sync >= 0.18
 
 
-def test_io_thread_auto_switches_both_ways_without_loss():
-    """``clusterapi.pool.io_thread: auto``: a burst above ``io_thread_on_rate``
+def test_io_thread_auto_switches_both_ways_without_loss(monkeypatch):
+    """``clusterapi.pool.io_thread: auto``: a burst above ``IO_THREAD_ON_RATE``
     hands the sockets to the I/O thread, a quiet spell hands them back; every
     notification is delivered exactly once across the switches, per pod in order."""
     import dataclasses
+    monkeypatch.setattr(NativeNotifierPool, "IO_THREAD_ON_RATE", 500.0)
+    monkeypatch.setattr(NativeNotifierPool, "IO_THREAD_OFF_RATE", 100.0)
 
     async def body():
         sink = StubSink(latency=0.002)  # responses lag: requests are in flight while switching
         await sink.start()
         m = Metrics(record_samples=True)
         s = settings(sink.url, depth=4)
-        s = dataclasses.replace(s, pool=dataclasses.replace(s.pool, io_thread_auto=True, io_thread_on_rate=500.0,
-                                                            io_thread_off_rate=100.0))
+        s = dataclasses.replace(s, pool=dataclasses.replace(s.pool, io_thread="auto"))
         pool = NativeNotifierPool(s, m)
         sent = []
         modes = []
@@ -451,22 +452,23 @@ def test_io_thread_auto_switches_both_ways_without_loss():
     assert all(seq == sorted(seq, key=order.get) for seq in by_uid.values())  # per pod in order
 
 
-def test_io_thread_auto_hands_back_with_requests_in_flight():
+def test_io_thread_auto_hands_back_with_requests_in_flight(monkeypatch):
     """The hand-back to the loop does not wait for a quiet queue: requests the
     thread sent are answered on the loop after the switch, none lost."""
     import dataclasses
+    monkeypatch.setattr(NativeNotifierPool, "IO_THREAD_ON_RATE", 500.0)
+    monkeypatch.setattr(NativeNotifierPool, "IO_THREAD_OFF_RATE", 100.0)
 
     async def body():
         sink = StubSink(latency=0.3)  # every response arrives well after the burst ends
         await sink.start()
         m = Metrics(record_samples=True)
         s = settings(sink.url, depth=64, connections=2)
-        s = dataclasses.replace(s, pool=dataclasses.replace(s.pool, io_thread_auto=True, io_thread_on_rate=500.0,
-                                                            io_thread_off_rate=100.0))
+        s = dataclasses.replace(s, pool=dataclasses.replace(s.pool, io_thread="auto"))
         pool = NativeNotifierPool(s, m)
         n = 0
         t_end = time.monotonic() + 0.5
-        while time.monotonic() < t_end:  # well above io_thread_on_rate even on a loaded machine
+        while time.monotonic() < t_end:  # well above IO_THREAD_ON_RATE even on a loaded machine
             for _ in range(3):
                 pool.submit(f"u{n}", "ADDED", "default", f"p{n}", core(f"u{n}"), 0, TS)
                 n += 1

@@ -640,12 +640,7 @@ def test_hub_framing_matches_pipeline_framing_on_random_chunking(seed, buf_bytes
     b.close()
 
 
-def test_reader_depth_setting():
-    from k8s_watcher_amd.utils.config import ConfigError, load_settings
-    assert load_settings("production", environ={}).watcher.watch_reader_depth == 2
-    for bad in (1, 9):
-        with pytest.raises(ConfigError):
-            load_settings("production", overrides={"watcher": {"watch_reader_depth": bad}}, environ={})
+def test_reader_depth_bounds():
     core = load().ReaderHub(16 * 1024, 4)
     with pytest.raises(ValueError):
         core.set_depth(9)
@@ -732,7 +727,7 @@ def test_runtime_log_level_reaches_every_hub_dispatched_scope():
         s = load_settings("staging", overrides={
             "clusterapi": {"base_url": sink.url, "health_check_on_start": False},
             "watcher": {"engine": "native", "namespace_scope": "discover", "watch_reader": "native",
-                        "hub_dispatch": True, "retry": {"delay_seconds": 0.05, "max_attempts": 0}}})
+                        "retry": {"delay_seconds": 0.05, "max_attempts": 0}}})
         log = logging.getLogger(SERVICE_LOGGER)
         old = log.level
         log.setLevel(logging.WARNING)

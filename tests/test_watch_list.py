@@ -15,7 +15,14 @@ from conftest import run
 from k8s_watcher_amd.testing.podgen import PodFactory
 from test_e2e_slice import check_schema, start_stack
 
-WL = {"watcher": {"initial_sync": "watch_list", "watch_list_idle_seconds": 0.5}}
+WL = {"watcher": {"initial_sync": "watch_list"}}
+
+
+@pytest.fixture(autouse=True)
+def _short_idle(monkeypatch):
+    """A server that never ends the initial events falls back after 0.5 s."""
+    from k8s_watcher_amd.engine import reflector
+    monkeypatch.setattr(reflector, "WATCH_LIST_IDLE_SECONDS", 0.5)
 
 
 @pytest.mark.parametrize("engine", ["native", "python"])
