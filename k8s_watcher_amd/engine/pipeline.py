@@ -148,10 +148,23 @@ class EventPipeline:
             elog.flush()
         return flush
 
-    def sync_native_log(self) -> None:
+    def log_flags_fn(self):
+        """A function giving this pipeline's event-log switches (log_events,
+        DEBUG on) now — a closure over the setting, the logger and the event
+        log only, shared by every scope that has the same three (the reader
+        hub evaluates it once per dispatch for all of them: net/reader.py)."""
+        setting, log, elog = self.log_events_setting, self.log, self.elog
+
+        def flags() -> tuple:
+            on = setting if setting is not None else log.isEnabledFor(logging.INFO)
+            return (on, on and elog.enabled(logging.DEBUG))
+        return flags
+
+    def sync_native_log(self, flags: Optional[tuple] = None) -> None:
         """Hand the event-log switches (log_events, DEBUG on) to the native side."""
-        log_events = self.log_events
-        flags = (log_events, log_events and self.elog.enabled(logging.DEBUG))
+        if flags is None:
+            log_events = self.log_events
+            flags = (log_events, log_events and self.elog.enabled(logging.DEBUG))
         if flags != self._native_log and self.native is not None:
             self.native.set_log(*flags)
             self._native_log = flags

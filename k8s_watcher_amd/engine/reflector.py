@@ -539,7 +539,9 @@ class Reflector:
         if (native is not None and framed[0]
                 and self.stream.bind_native(native, on_native, pipeline.shared_flush(),
                                             (id(pipeline.notifier), id(pipeline.elog)),
-                                            sync=pipeline.sync_native_log)):
+                                            sync=pipeline.sync_native_log,
+                                            sync_group=((id(pipeline.elog), pipeline.log_events_setting),
+                                                        pipeline.log_flags_fn()))):
             self._rv_native = native.last_rv
             pipeline.sync_native_log()
             self.metrics.c["watches_hub_dispatch"] += 1

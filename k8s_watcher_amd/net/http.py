@@ -601,9 +601,15 @@ class StreamResponse:
 
     @property
     def last_activity(self) -> float:
-        return self._proto.last_activity
+        p = self._proto
+        hub = getattr(p, "hub", None)
+        if hub is not None and getattr(p, "hub_sid", None) is not None:
+            # a hub-read stream: its reads are timed by the hub (bound ones
+            # never pass through Python per read)
+            return max(p.last_activity, hub.last_read(p.hub_sid))
+        return p.last_activity
 
-    def bind_native(self, pipeline_core, on_result, flush, flush_key, sync=None) -> bool:
+    def bind_native(self, pipeline_core, on_result, flush, flush_key, sync=None, sync_group=None) -> bool:
         """A hub-read watch body (net/reader.py) goes straight from the hub's
         buffers into the fused native ``pipeline_core`` — no Python call per
         socket read; ``on_result(result, read_ns, body_done)`` gets only the
@@ -615,7 +621,7 @@ class StreamResponse:
         if (hub is None or parser.state != ResponseParser.RAW or parser.buf or p.stream_sink is None
                 or p.closed.done()):
             return False
-        hub.bind(p, pipeline_core, parser.raw_chunked, on_result, flush, flush_key, sync)
+        hub.bind(p, pipeline_core, parser.raw_chunked, on_result, flush, flush_key, sync, sync_group)
         return p.hub_result is not None
 
     def close(self) -> None:

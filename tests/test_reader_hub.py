@@ -69,6 +69,26 @@ def test_hub_reads_streams_in_order_and_signals_eof():
         b.close()
 
 
+def test_last_read_times_a_streams_reads():
+    """last_read(sid): when the stream's last read with bytes ended, on
+    time.monotonic()'s clock (the reflectors' idle checks of bound streams,
+    which never pass through Python per read); 0.0 before any, and for an
+    unknown stream."""
+    core = load().ReaderHub(64 * 1024, 4)
+    a, b = socket.socketpair()
+    sid = core.add(os.dup(b.fileno()))
+    assert core.last_read(sid) == 0.0 and core.last_read(sid + 99) == 0.0
+    t0 = time.monotonic()
+    a.sendall(b"x" * 1000)
+    got, _ = _drain(core, 1000)
+    t1 = time.monotonic()
+    assert len(got[sid]) == 1000
+    assert t0 <= core.last_read(sid) <= t1
+    core.close()
+    a.close()
+    b.close()
+
+
 def test_hub_pause_stops_reading_and_remove_closes():
     mod = load()
     core = mod.ReaderHub(64 * 1024, 2)
@@ -875,6 +895,7 @@ def test_dispatch_delivery_is_sliced_across_loop_turns_in_order():
         hub.core = Core([(first, list(range(200))), (second, [7])])
         hub.protos = {sid: Proto(log, sid) for sid in range(200)}
         hub._flush, hub._pending, hub._soon, hub.closed = {"k": lambda: turns.append(len(log))}, None, None, False
+        hub._groups = {}
         hub._on_ready()
         assert hub._pending is not None and hub.core.takes == 1 and len(log) < 200
         n = len(log)
