@@ -70,6 +70,8 @@ GC_FREEZE = True
 # watch, whose reader thread is the bound (profiles/r5/framing_ab,
 # r5/framing_many); on | off for tests
 HUB_FRAMING = "auto"
+# reader-hub threads: 0 = auto (utils/cpus.py auto_reader_threads)
+HUB_READERS = 0
 MALLOC_TRIM_MIN_FREE = 16 << 20  # a periodic malloc_trim runs only when the C heap keeps this much free
 SPOOL_REPLAY_BATCH = 1000  # owed notifications re-submitted from the spool per replay pass
 
@@ -352,12 +354,13 @@ class WatcherService:
                                                        or getattr(http.ssl_context, "kw_tls", None) is not None):
                 # watch bodies read (and, for https, decrypted) on a native thread (net/reader.py)
                 from ..net.reader import WatchReaderHub
-                from ..utils.cpus import auto_tls_threads
+                from ..utils.cpus import auto_reader_threads, auto_tls_threads
                 self._reader_hub = WatchReaderHub(s.watcher.watch_read_bytes or (4 << 20),
                                                   s.watcher.watch_reader_buffers,
                                                   max_bytes=s.watcher.watch_reader_max_bytes,
                                                   frame=(HUB_FRAMING == "on" or
                                                          (HUB_FRAMING == "auto" and self._multi)),
+                                                  readers=HUB_READERS or auto_reader_threads(self._multi),
                                                   tls_records=s.watcher.watch_tls_records == "native",
                                                   tls_threads=(s.watcher.watch_tls_threads
                                                                if s.watcher.watch_tls_threads >= 0
@@ -806,6 +809,9 @@ class WatcherService:
         # core and it waited 5.8 ms/s for a CPU (profiles/r6/tls_timeline)
         if self._reader_hub is not None:
             tids += list(self._reader_hub.core.tls_thread_ids())
+            # reader threads past the first run beside the workers (the first
+            # gets a core of its own below)
+            tids += list(self._reader_hub.core.thread_ids())[1:]
         reader_cpus = None
         reader_tid = self._reader_hub.core.thread_id() if self._reader_hub is not None else 0
         if reader_tid and mode == "auto":

@@ -38,16 +38,19 @@ class WatchReaderHub:
 
     def __init__(self, buf_bytes: int, nbufs: int = 64,
                  loop: Optional[asyncio.AbstractEventLoop] = None, max_bytes: int = 0, frame: bool = True,
-                 depth: int = 2, tls_records: bool = True, tls_threads: int = 0) -> None:
+                 depth: int = 2, tls_records: bool = True, tls_threads: int = 0, readers: int = 1) -> None:
         self.loop = loop or asyncio.get_running_loop()
         # max_bytes: read-ahead over all streams (0: the whole pool); frame: the
         # hub's thread de-chunks and splits bound bodies (watcher.hub_framing)
         self.frame = bool(frame)
         self.core = native.load().ReaderHub(max(64 * 1024, int(buf_bytes)), max(2, int(nbufs)),
                                             max(0, int(max_bytes)), frame=self.frame)
-        # depth: buffers read ahead per stream (watcher.watch_reader_depth)
+        # depth: buffers read ahead per stream
         if depth != 2:
             self.core.set_depth(int(depth))
+        # readers: threads polling the streams (each stream stays with one)
+        if readers > 1:
+            self.core.set_readers(int(readers))
         # https watches: the hub opens TLS 1.3 records itself, on a pool of
         # tls_threads besides the reader thread (watcher.watch_tls_records /
         # watch_tls_threads; ops/csrc/tls13.inc)

@@ -36,9 +36,11 @@ def _drain(core, want_bytes, timeout=5.0):
     return got, ends
 
 
-def test_hub_reads_streams_in_order_and_signals_eof():
+@pytest.mark.parametrize("readers", [1, 3])
+def test_hub_reads_streams_in_order_and_signals_eof(readers):
     mod = load()
     core = mod.ReaderHub(64 * 1024, 4)
+    assert core.set_readers(readers) and len(core.thread_ids()) == readers
     pairs = [socket.socketpair() for _ in range(3)]
     sids = [core.add(os.dup(b.fileno())) for a, b in pairs]
     payload = {sid: os.urandom(300_000) for sid in sids}  # several buffers each
@@ -293,7 +295,8 @@ def test_read_ahead_is_capped_in_bytes_over_all_streams():
         b.close()
 
 
-def test_take_and_remove_race_the_reader_thread():
+@pytest.mark.parametrize("readers", [1, 3])
+def test_take_and_remove_race_the_reader_thread(readers):
     """The hub thread recv()s outside its lock. Under a steady flood on many
     streams, takes that land while it is appending to an entry, releases, and
     removals of streams it is reading must keep every stream's bytes a gap-free,
@@ -302,6 +305,7 @@ def test_take_and_remove_race_the_reader_thread():
     import threading
     mod = load()
     core = mod.ReaderHub(64 * 1024, 16)
+    core.set_readers(readers)  # several threads: streams spread over them, each stays with one
     pairs = [socket.socketpair() for _ in range(12)]
     for a, _b in pairs:
         a.setblocking(True)
@@ -911,3 +915,67 @@ def test_dispatch_delivery_is_sliced_across_loop_turns_in_order():
         assert len(turns) >= 3  # flushed after every turn
 
     run(main())
+
+
+def test_set_readers_bounds_and_spread():
+    """set_readers: 1..8 threads, never fewer than running; streams added
+    after it go to the thread with the fewest (thread_ids names them all)."""
+    core = load().ReaderHub(64 * 1024, 8)
+    with pytest.raises(ValueError):
+        core.set_readers(0)
+    with pytest.raises(ValueError):
+        core.set_readers(9)
+    assert core.set_readers(2) and core.set_readers(2)
+    assert not core.set_readers(1)  # threads never go away while the hub runs
+    ids = core.thread_ids()
+    assert len(ids) == 2 and len(set(ids)) == 2 and all(ids)
+    core.close()
+
+
+def test_service_spreads_namespace_watches_over_reader_threads(monkeypatch):
+    """Several namespace scopes with two reader threads (engine/service.py
+    HUB_READERS; auto gives two on a CPU share of 12+): every pod of every
+    namespace is notified once, the hub runs two threads."""
+    from conftest import run
+    from k8s_watcher_amd.engine import service
+    from k8s_watcher_amd.engine.service import WatcherService
+    from k8s_watcher_amd.kube.kubeconfig import KubeEndpoint
+    from k8s_watcher_amd.metrics import Metrics
+    from k8s_watcher_amd.testing.fake_apiserver import FakeApiServer
+    from k8s_watcher_amd.testing.podgen import PodFactory
+    from k8s_watcher_amd.testing.stub_sink import StubSink
+    from k8s_watcher_amd.utils.config import load_settings
+
+    monkeypatch.setattr(service, "HUB_READERS", 2)
+    names = [f"ns-{i}" for i in range(6)]
+
+    async def body():
+        srv = FakeApiServer(namespaces=names)
+        await srv.start()
+        sink = StubSink()
+        await sink.start()
+        s = load_settings("staging", overrides={
+            "clusterapi": {"base_url": sink.url, "health_check_on_start": False},
+            "watcher": {"engine": "native", "namespace_scope": "discover",
+                        "retry": {"delay_seconds": 0.05, "max_attempts": 0}}}, environ={})
+        svc = WatcherService(s, endpoint=KubeEndpoint(server=srv.url), metrics=Metrics())
+        try:
+            await svc.start()
+            f = PodFactory(seed=5, namespaces=names)
+            for _ in range(5):
+                for ns in names:
+                    srv.create(f.new_pod(namespace=ns))
+            await sink.state.wait_for(30, timeout=15)
+            readers = len(svc._reader_hub.core.thread_ids())
+            got = sink.state.payloads()
+        finally:
+            svc.stop()
+            await svc.shutdown()
+            await sink.stop()
+            await srv.stop()
+        return readers, got
+
+    readers, got = run(body(), timeout=60)
+    assert readers == 2
+    keys = [(p["uid"], p["event_type"]) for p in got]
+    assert len(keys) == 30 and len(set(keys)) == 30

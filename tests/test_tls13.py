@@ -566,7 +566,8 @@ def test_ring_memory_is_counted_in_the_pool_and_shrinks_with_the_class(pki):
     srv.close()
 
 
-def test_many_tls_streams_share_the_pool_with_their_rings(pki):
+@pytest.mark.parametrize("readers", [1, 2])
+def test_many_tls_streams_share_the_pool_with_their_rings(pki, readers):
     """Sixteen https streams on a 1 MiB pool: rings and buffers together
     stay near the pool's memory, and every stream is delivered whole (a
     stream's first buffer never waits behind rings)."""
@@ -595,6 +596,7 @@ def test_many_tls_streams_share_the_pool_with_their_rings(pki):
         t.start()
     hub = mod.ReaderHub(256 << 10, 4)
     hub.set_tls(True, 2)
+    hub.set_readers(readers)  # two reader threads share the one CryptoPool (one batch at a time)
     ctx = mod.TlsContext(ca_pem=open(pki.ca_crt, "rb").read())
     sids = {}
     for i in range(n):
