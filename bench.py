@@ -520,6 +520,9 @@ PROGRESS = [False]
 
 async def rank_main(args, d: Dist) -> dict:
     from k8s_watcher_amd.engine.service import WatcherService
+    if os.environ.get("BENCH_HUB_READERS"):  # A/B of the reader-hub thread count (service.HUB_READERS)
+        from k8s_watcher_amd.engine import service as _service
+        _service.HUB_READERS = int(os.environ["BENCH_HUB_READERS"])
     from k8s_watcher_amd.kube.kubeconfig import KubeEndpoint
     from k8s_watcher_amd.metrics import Metrics
     from k8s_watcher_amd.testing.cluster_replay import namespace_names

@@ -70,8 +70,13 @@ GC_FREEZE = True
 # watch, whose reader thread is the bound (profiles/r5/framing_ab,
 # r5/framing_many); on | off for tests
 HUB_FRAMING = "auto"
-# reader-hub threads: 0 = auto (utils/cpus.py auto_reader_threads)
-HUB_READERS = 0
+# reader-hub threads (net/reader.py; readerhub.inc set_readers). One: at 64
+# namespace watches on the box's 16-CPU share two readers took the reader
+# thread off the bound (recv 0.97 -> 0.8-0.97 over two) but the loop then
+# saturated (0.97-0.99) and the decode workers, sharing cores with the second
+# reader, ran slower: 2.30-2.42M against 2.31-2.53M with one
+# (profiles/r6/readers). More pays only where the loop has room.
+HUB_READERS = 1
 MALLOC_TRIM_MIN_FREE = 16 << 20  # a periodic malloc_trim runs only when the C heap keeps this much free
 SPOOL_REPLAY_BATCH = 1000  # owed notifications re-submitted from the spool per replay pass
 
@@ -354,13 +359,13 @@ class WatcherService:
                                                        or getattr(http.ssl_context, "kw_tls", None) is not None):
                 # watch bodies read (and, for https, decrypted) on a native thread (net/reader.py)
                 from ..net.reader import WatchReaderHub
-                from ..utils.cpus import auto_reader_threads, auto_tls_threads
+                from ..utils.cpus import auto_tls_threads
                 self._reader_hub = WatchReaderHub(s.watcher.watch_read_bytes or (4 << 20),
                                                   s.watcher.watch_reader_buffers,
                                                   max_bytes=s.watcher.watch_reader_max_bytes,
                                                   frame=(HUB_FRAMING == "on" or
                                                          (HUB_FRAMING == "auto" and self._multi)),
-                                                  readers=HUB_READERS or auto_reader_threads(self._multi),
+                                                  readers=HUB_READERS,
                                                   tls_records=s.watcher.watch_tls_records == "native",
                                                   tls_threads=(s.watcher.watch_tls_threads
                                                                if s.watcher.watch_tls_threads >= 0

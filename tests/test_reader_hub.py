@@ -934,8 +934,8 @@ def test_set_readers_bounds_and_spread():
 
 def test_service_spreads_namespace_watches_over_reader_threads(monkeypatch):
     """Several namespace scopes with two reader threads (engine/service.py
-    HUB_READERS; auto gives two on a CPU share of 12+): every pod of every
-    namespace is notified once, the hub runs two threads."""
+    HUB_READERS): every pod of every namespace is notified once, the hub
+    runs two threads."""
     from conftest import run
     from k8s_watcher_amd.engine import service
     from k8s_watcher_amd.engine.service import WatcherService
