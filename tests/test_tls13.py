@@ -61,11 +61,11 @@ def _drain(hub, sid, timeout=30.0):
     return bytes(got), end
 
 
-def _native_server(pki, srv, body_parts, threads=2, key_update_at=None, forge=False, result=None):
+def _native_server(pki, srv, body_parts, threads=2, key_update_at=None, forge=False, result=None, **ctx_kw):
     """Serve one connection with the fixture's native TLS server: read the
     request, then send the parts (a KeyUpdate before part ``key_update_at``),
     then close_notify (or a forged record)."""
-    tls = load().TlsServerContext(pki.server_crt, pki.server_key, threads=threads)
+    tls = load().TlsServerContext(pki.server_crt, pki.server_key, threads=threads, **ctx_kw)
     c, _ = srv.accept()
     conn = tls.accept(c.detach())
     req = b""
@@ -114,6 +114,40 @@ def test_large_body_opened_in_parallel_is_byte_exact_across_a_key_update(pki, th
     if threads:  # big reads went to the pool, and its threads did open records
         assert st["tls_pooled_records"] > 0 and sum(n for _, n in st["tls_pool"][1:]) > 0
     assert sum(n for _, n in res["pool"]) > 0  # the server sealed on its pool too
+    hub.close()
+    srv.close()
+
+
+@pytest.mark.parametrize("ring_budget", [2 << 30, 0])
+def test_large_sends_through_the_sendfile_ring_wrap_byte_exact(pki, ring_budget):
+    """The fixture's sender seals large sends into a memfd ring and sends them
+    with sendfile; a region is sealed over only once the peer has read it.
+    Many times the ring's size, with a key update and small (copied) sends
+    interleaved, arrives byte-exact; with no ring budget every send is copied."""
+    big = [os.urandom(4 << 20) for _ in range(3)]
+    parts = []
+    for i in range(30):  # 120 MiB in 4 MiB sends: several turns of the ring
+        parts.append(big[i % 3])
+        if i % 7 == 3:
+            parts.append(b"small-%d;" % i)  # below RING_MIN_SEND: the copy path, in order
+    want = b"".join(parts)
+    srv = _listener()
+    res = {}
+    t = threading.Thread(target=_native_server, args=(pki, srv, parts),
+                         kwargs={"key_update_at": 12, "result": res, "ring_budget": ring_budget})
+    t.start()
+    hub = load().ReaderHub(1 << 20, 8)
+    hub.set_tls(True, 2)
+    sid = _client(hub, pki, srv.getsockname()[1])
+    got, end = _drain(hub, sid, timeout=120)
+    t.join()
+    assert end == 0 and len(got) == len(want) and got == want
+    assert hub.stats()["tls_key_updates"] == 1
+    st = res["stats"]
+    if ring_budget:
+        assert st["ring_bytes"] >= 29 * (4 << 20)  # every large send went through the ring
+    else:
+        assert st["ring_bytes"] == 0
     hub.close()
     srv.close()
 
