@@ -58,7 +58,8 @@ def test_reader_hub_on_host():
     """The native watch reader's contract (order, EOF, pause, pool backpressure) on the host's CPUs."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import test_reader_hub
-    test_reader_hub.test_hub_reads_streams_in_order_and_signals_eof()
+    for readers in (1, 3):
+        test_reader_hub.test_hub_reads_streams_in_order_and_signals_eof(readers)
     test_reader_hub.test_hub_pause_stops_reading_and_remove_closes()
     test_reader_hub.test_pool_exhaustion_is_backpressure_not_loss()
     test_reader_hub.test_http_stream_adopted_by_hub_end_to_end()
@@ -66,7 +67,8 @@ def test_reader_hub_on_host():
         test_reader_hub.test_read_ahead_is_capped_per_stream(depth)
     test_reader_hub.test_read_ahead_is_capped_in_bytes_over_all_streams()
     # the thread recv()s outside its lock: takes and removals racing it, on the host's cores
-    test_reader_hub.test_take_and_remove_race_the_reader_thread()
+    for readers in (1, 3):  # one reader thread, and three sharing the streams
+        test_reader_hub.test_take_and_remove_race_the_reader_thread(readers)
 
 
 def test_hub_framing_and_grouped_dispatch_on_host():
