@@ -48,7 +48,7 @@ def parse_args(argv=None):
     ap.add_argument("--pods", type=int, default=100000, help="pods in the whole cluster")
     ap.add_argument("--scope", default="discover", choices=["discover", "cluster"])
     ap.add_argument("--churn", type=int, default=1000, help="pods finished, deleted and created while expired")
-    ap.add_argument("--slice-ms", type=float, default=4.0, help="watcher.relist_slice_ms")
+    ap.add_argument("--slice-ms", type=float, default=4.0, help="engine/reflector.py RELIST_SLICE_MS (loop time per relist slice)")
     ap.add_argument("--concurrency", type=int, default=16, help="watcher.relist_concurrency")
     ap.add_argument("--page", type=int, default=500, help="watcher.list_page_size")
     ap.add_argument("--decode-threads", default="auto")
@@ -244,7 +244,9 @@ async def wait_quiet(svc, c, relists_target: int, timeout: float) -> None:
 
 
 async def main_async(args) -> dict:
+    from k8s_watcher_amd.engine import reflector as _reflector
     from k8s_watcher_amd.engine.service import WatcherService
+    _reflector.RELIST_SLICE_MS = args.slice_ms  # (a fixed choice since round 6: the A/B knob of this benchmark)
     from k8s_watcher_amd.kube.kubeconfig import KubeEndpoint
     from k8s_watcher_amd.metrics import Metrics
     from k8s_watcher_amd.testing.stub_sink import _GEN  # noqa: F401  (same key format as payload_key)
@@ -277,7 +279,7 @@ async def main_async(args) -> dict:
             "clusterapi": {"base_url": f"http://127.0.0.1:{sink_port}", "timeout": 30},
             "watcher": {"engine": "native", "log_level": "WARNING", "retry": {"max_attempts": 0, "delay_seconds": 0.05},
                         "namespace_scope": "discover" if args.scope == "discover" else "client",
-                        "list_page_size": args.page, "relist_slice_ms": args.slice_ms,
+                        "list_page_size": args.page,
                         "relist_concurrency": args.concurrency, "decode_threads": args.decode_threads,
                         "initial_sync": args.initial_sync}},
             environ={})
