@@ -163,3 +163,21 @@ def test_loop_lag_probe_sees_a_blocked_loop():
     # the shared CPU may preempt the loop (or the ticker) now and then, more
     # so under a parallel test run: most idle ticks are answered fast
     assert idle["over_1ms"] <= max(3, idle["n"] // 10) and idle["mean_us"] < 1000, idle
+
+
+def test_set_overrides_fold_into_one_nested_dict():
+    """bench --set KEY=VALUE (repeatable, main.py --set's syntax): every
+    per-setting bench flag of earlier rounds is one of these now (round-6
+    pruning: 63 -> 45 flags)."""
+    args = bench.parse_args(["--set", "clusterapi.pool.io_thread=on", "--set", "watcher.watch_tls_threads=5",
+                             "--set", "watcher.thread_pinning=none", "--set", "watcher.validate=full"])
+    ov = bench.set_overrides(args)
+    # values are YAML (as main.py --set): "on" is true, which io_thread reads as "on"
+    assert ov == {"clusterapi": {"pool": {"io_thread": True}},
+                  "watcher": {"watch_tls_threads": 5, "thread_pinning": "none", "validate": "full"}}
+    assert bench.set_value(args, "watcher.thread_pinning", "auto") == "none"
+    assert bench.set_value(args, "watcher.decode_threads", "auto") == "auto"
+    assert bench.set_value(bench.parse_args([]), "watcher.thread_pinning", "auto") == "auto"
+    import re
+    flags = re.findall(r'add_argument\("(--[a-z0-9-]+)"', open(bench.__file__).read())
+    assert 40 <= len(flags) <= 50, len(flags)
