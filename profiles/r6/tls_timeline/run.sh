@@ -11,7 +11,7 @@ for r in "$@"; do
   i=$((i+1))
   case $r in
     tls) X="--api-tls";; plain) X="";;
-    tlsboth) X="--api-tls --tls";;
+    tlsboth) X="--api-tls --tls";; tlssink) X="--tls";;
     tlsapart) X="--api-tls --fixture-placement apart";; plainapart) X="--fixture-placement apart";;
     tls64) X="--api-tls --watch-scope discover --namespaces 64";; plain64) X="--watch-scope discover --namespaces 64";;
     r1m32) X="--watch-scope discover --namespaces 64 --set watcher.watch_reader_max_bytes=33554432"; export BENCH_HUB_READERS=1;;
