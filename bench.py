@@ -596,6 +596,13 @@ async def rank_main(args, d: Dist) -> dict:
             endpoint = KubeEndpoint(server=f"http://127.0.0.1:{shared['api_port']}")
         svc = WatcherService(settings, endpoint=endpoint, metrics=metrics)
         await svc.start()
+        if os.environ.get("BENCH_READERS_SHARE_CORE") and getattr(svc, "_reader_hub", None) is not None:
+            # A/B: every reader thread on the first one's core (its SMT siblings), not beside the workers
+            _tids = svc._reader_hub.core.thread_ids()
+            if len(_tids) > 1:
+                _cpus = os.sched_getaffinity(_tids[0])
+                for _t in _tids[1:]:
+                    os.sched_setaffinity(_t, _cpus)
         mine = sorted(r.namespace for r in svc.reflectors if r.namespace) if scope == "discover" else ["*"]
         per_step = (shared["events_per_step"] if mine == ["*"]
                     else sum(shared["ns_events"][ns] for ns in mine))
