@@ -168,6 +168,16 @@ def test_bench_https_api_server_through_the_native_reader():
     assert d["watch_reader_rank0"]["mode"] == "native" and d["watch_reader_rank0"]["reads"] > 0
     assert d["watch_reader_rank0"]["hub_dispatch_watches"] > 0  # TLS watches are fed natively too
     assert d["per_rank"][0]["events"] == 2 * 1500
+    # the per-stage timeline (profiles/r6/tls_timeline): the reader's waits and the fixture's
+    # senders (sealing, queue waits, writer idle / in send / waiting for the socket) over the
+    # timed steps, from the replay fixture's TLSSTATS
+    timed = d["watch_reader_rank0"]["timed"]
+    assert set(timed["waits"]) == {"starved", "held_waits", "over_budget"}
+    tls = timed["tls"]
+    assert tls["taken"] >= 1 and 0 <= tls["reader_idle_frac"] and 0 <= tls["pool_wait_frac"]
+    assert set(tls["fixture"]) >= {"seal_frac", "push_frac", "idle_frac", "send_frac", "pollout_frac",
+                                   "sendfile_share"}
+    assert tls["fixture"]["seal_frac"] > 0
 
 
 def test_balanced_assignment_bounded_and_stable():
