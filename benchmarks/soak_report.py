@@ -79,6 +79,34 @@ def main(argv=None) -> None:
         life = max(1e-9, (mine[-1]["t"] - t0) / 3600)
         for k in keys:
             out.append(f"| `{k}` | {int(at1[k]):,} | {int(mine[-1][k]):,} | {mine[-1][k] / life:,.0f} |")
+    tr = s.get("transport") or {}
+    if tr.get("api_server") == "https" or tr.get("clusterapi") == "https":
+        out.append("")
+        out.append(f"**Transport**: API server {tr.get('api_server')}, clusterapi {tr.get('clusterapi')}"
+                   + (f", a KeyUpdate every {tr['key_update_mib']:g} MiB per connection" if tr.get("key_update_mib") else "")
+                   + ".")
+        fr = tr.get("front") or {}
+        if fr:
+            out.append("")
+            out.append(f"- TLS front: {fr.get('connections', 0):,} connections, "
+                       f"{fr.get('bytes_down', 0) / 1e9:,.1f} GB sealed to the watcher, "
+                       f"{fr.get('key_updates', 0):,} KeyUpdates and {fr.get('tickets', 0):,} session tickets sent "
+                       f"(half of them split over two records), {fr.get('errors', 0)} errors")
+        procs = tr.get("watcher_key_updates_by_process") or []
+        if procs:
+            ku = [int(p.get("key_updates", 0)) for p in procs]
+            nat = sum(int(p.get("streams_native", 0)) for p in procs)
+            ossl = sum(int(p.get("streams_openssl", 0)) for p in procs)
+            out.append(f"- watcher processes: {len(procs)}, every one followed key updates "
+                       f"({min(ku):,}-{max(ku):,} each)" if min(ku) > 0 else
+                       f"- watcher processes: {len(procs)}, key updates per process {min(ku):,}-{max(ku):,}")
+            out.append(f"- watch streams whose records the hub opened itself: {nat:,}; left on SSL_read: {ossl:,}")
+        if "watch_tls_key_updates" in mine[-1]:
+            at1 = next((x for x in mine if x["t"] - t0 >= 3600), mine[-1])
+            life = max(1e-9, (mine[-1]["t"] - t0) / 3600)
+            out.append(f"- last process: {int(at1['watch_tls_key_updates']):,} key updates at +1 h, "
+                       f"{int(mine[-1]['watch_tls_key_updates']):,} at the end "
+                       f"({mine[-1]['watch_tls_key_updates'] / life:,.0f} per hour)")
     og = s.get("object_growth")
     if og:
         out.append("")

@@ -20,6 +20,8 @@ for r in "$@"; do
     r1) X="--watch-scope discover --namespaces 64"; export BENCH_HUB_READERS=1;;
     r2smt) X="--watch-scope discover --namespaces 64"; export BENCH_HUB_READERS=2 BENCH_READERS_SHARE_CORE=1;;
     r1b) X="--watch-scope discover --namespaces 64"; export BENCH_HUB_READERS=1; unset BENCH_READERS_SHARE_CORE;;
+    p1) X="--watch-scope discover --namespaces 64 --probe"; export BENCH_HUB_READERS=1; unset BENCH_READERS_SHARE_CORE;;
+    p2) X="--watch-scope discover --namespaces 64 --probe"; export BENCH_HUB_READERS=2; unset BENCH_READERS_SHARE_CORE;;
     tls64r1) X="--api-tls --watch-scope discover --namespaces 64"; export BENCH_HUB_READERS=1;;
     tls64r2) X="--api-tls --watch-scope discover --namespaces 64"; export BENCH_HUB_READERS=2;;
     *) echo "unknown run $r"; exit 2;;
