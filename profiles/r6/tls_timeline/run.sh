@@ -20,6 +20,15 @@ for r in "$@"; do
     r1) X="--watch-scope discover --namespaces 64"; export BENCH_HUB_READERS=1;;
     r2smt) X="--watch-scope discover --namespaces 64"; export BENCH_HUB_READERS=2 BENCH_READERS_SHARE_CORE=1;;
     r1b) X="--watch-scope discover --namespaces 64"; export BENCH_HUB_READERS=1; unset BENCH_READERS_SHARE_CORE;;
+    p1) X="--watch-scope discover --namespaces 64 --probe"; export BENCH_HUB_READERS=1; unset BENCH_READERS_SHARE_CORE;;
+    p2) X="--watch-scope discover --namespaces 64 --probe"; export BENCH_HUB_READERS=2; unset BENCH_READERS_SHARE_CORE;;
+    ns0) X="--watch-scope discover --namespaces 64 --probe"; export BENCH_HUB_READERS=1; unset BENCH_READERS_SHARE_CORE;;
+    ns32) X="--watch-scope discover --namespaces 64 --probe --set watcher.watch_reader_max_bytes=33554432"; export BENCH_HUB_READERS=1; unset BENCH_READERS_SHARE_CORE;;
+    ns16) X="--watch-scope discover --namespaces 64 --probe --set watcher.watch_reader_max_bytes=16777216"; export BENCH_HUB_READERS=1; unset BENCH_READERS_SHARE_CORE;;
+    r2ns16) X="--watch-scope discover --namespaces 64 --probe --set watcher.watch_reader_max_bytes=16777216"; export BENCH_HUB_READERS=2; unset BENCH_READERS_SHARE_CORE;;
+    r2ns8) X="--watch-scope discover --namespaces 64 --probe --set watcher.watch_reader_max_bytes=8388608"; export BENCH_HUB_READERS=2; unset BENCH_READERS_SHARE_CORE;;
+    cl0) X="--probe"; export BENCH_HUB_READERS=1;;
+    cl32) X="--probe --set watcher.watch_reader_max_bytes=33554432"; export BENCH_HUB_READERS=1;;
     tls64r1) X="--api-tls --watch-scope discover --namespaces 64"; export BENCH_HUB_READERS=1;;
     tls64r2) X="--api-tls --watch-scope discover --namespaces 64"; export BENCH_HUB_READERS=2;;
     *) echo "unknown run $r"; exit 2;;
