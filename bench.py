@@ -450,6 +450,14 @@ class Fixtures:
             shutil.rmtree(self.verify_dir, ignore_errors=True)
 
 
+def hub_streams(svc) -> list:
+    """Each hub-read stream's polling state (readerhub.inc stream_state), for a stalled step's report."""
+    hub = getattr(svc, "_reader_hub", None)
+    if hub is None or hub.closed:
+        return []
+    return [(sid, tuple(hub.core.stream_state(sid))) for sid in sorted(hub.protos)]
+
+
 def set_overrides(args) -> dict:
     """--set KEY=VALUE expressions (repeatable) as one nested override dict,
     applied over the bench's own (main.py --set's syntax: utils/config.py)."""
@@ -656,7 +664,8 @@ async def rank_main(args, d: Dist) -> dict:
                     raise TimeoutError(f"rank {d.rank} step {k}: {c['events_received'] - base}/{expect} events, "
                                        f"{svc.notifier.outstanding()} notifications outstanding; streams "
                                        f"{[(r.scope, r.watch_count, r.rv) for r in svc.reflectors]}; "
-                                       f"counters { {n: v for n, v in c.items() if v and 'latency' not in n} }")
+                                       f"counters { {n: v for n, v in c.items() if v and 'latency' not in n} }; "
+                                       f"hub {hub_streams(svc)}")
                 await asyncio.sleep(0.0005)
             t_end = time.perf_counter()
             if sent is not None:

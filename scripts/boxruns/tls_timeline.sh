@@ -27,6 +27,8 @@ for r in "$@"; do
     ns16) X="--watch-scope discover --namespaces 64 --probe --set watcher.watch_reader_max_bytes=16777216"; export BENCH_HUB_READERS=1; unset BENCH_READERS_SHARE_CORE;;
     r2ns16) X="--watch-scope discover --namespaces 64 --probe --set watcher.watch_reader_max_bytes=16777216"; export BENCH_HUB_READERS=2; unset BENCH_READERS_SHARE_CORE;;
     r2ns8) X="--watch-scope discover --namespaces 64 --probe --set watcher.watch_reader_max_bytes=8388608"; export BENCH_HUB_READERS=2; unset BENCH_READERS_SHARE_CORE;;
+    d64) X="--watch-scope discover --namespaces 64"; export BENCH_HUB_READERS=1; unset BENCH_READERS_SHARE_CORE;;
+    r2m8) X="--watch-scope discover --namespaces 64 --set watcher.watch_reader_max_bytes=8388608"; export BENCH_HUB_READERS=2; unset BENCH_READERS_SHARE_CORE;;
     cl0) X="--probe"; export BENCH_HUB_READERS=1;;
     cl32) X="--probe --set watcher.watch_reader_max_bytes=33554432"; export BENCH_HUB_READERS=1;;
     tls64r1) X="--api-tls --watch-scope discover --namespaces 64"; export BENCH_HUB_READERS=1;;

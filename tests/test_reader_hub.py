@@ -979,3 +979,55 @@ def test_service_spreads_namespace_watches_over_reader_threads(monkeypatch):
     assert readers == 2
     keys = [(p["uid"], p["event_type"]) for p in got]
     assert len(keys) == 30 and len(set(keys)) == 30
+
+
+@pytest.mark.parametrize("readers,seed", [(1, 0), (1, 1), (2, 0), (2, 1)])
+def test_starved_streams_are_all_woken_when_bytes_wait(readers, seed):
+    """Many streams over a one-buffer read-ahead budget, in rounds: a few
+    streams send a lot, most send a few hundred bytes (and drain at once),
+    the consumer takes everything before the next round. A stream disarmed
+    over the budget is re-armed as buffers come back; a re-armed stream whose
+    socket was drained gets no event, so it must not use up the wake-ups —
+    before round 6's fix the streams still holding bytes stayed disarmed once
+    every buffer was back (stalled in every one of these cases, one reader or
+    two; a 64-namespace bench with an 8 MiB read-ahead hung on the box)."""
+    import random
+    import threading
+    rng = random.Random(seed)
+    n = 48
+    core = load().ReaderHub(64 << 10, 64, 64 << 10)
+    core.set_readers(readers)
+    pairs = [socket.socketpair() for _ in range(n)]
+    for a, _b in pairs:
+        a.setblocking(True)
+    sids = [core.add(os.dup(b.fileno())) for _a, b in pairs]
+    idx = {sid: i for i, sid in enumerate(sids)}
+    got = [0] * n
+    try:
+        for r in range(30):
+            sizes = [rng.choice((0, 300, 300, 300, 300, 300, 150_000)) for _ in range(n)]
+            want = [g + s for g, s in zip(got, sizes)]
+            ths = [threading.Thread(target=a.sendall, args=(b"y" * s,)) for (a, _b), s in zip(pairs, sizes) if s]
+            for t in ths:
+                t.start()
+            last = time.monotonic()
+            while got != want:
+                items = core.take()
+                for sid, buf, view, _ns, _err in items:
+                    if view is not None:
+                        got[idx[sid]] += len(view)
+                        view.release()
+                        core.release(buf)
+                if items:
+                    last = time.monotonic()
+                else:
+                    stalled = [(i, want[i] - got[i], core.stream_state(sids[i])) for i in range(n) if got[i] != want[i]]
+                    assert time.monotonic() - last < 3.0, f"round {r}: stalled {stalled[:4]}"
+                time.sleep(0.0003)
+            for t in ths:
+                t.join()
+    finally:
+        core.close()
+        for a, b in pairs:
+            a.close()
+            b.close()
