@@ -70,13 +70,19 @@ GC_FREEZE = True
 # watch, whose reader thread is the bound (profiles/r5/framing_ab,
 # r5/framing_many); on | off for tests
 HUB_FRAMING = "auto"
-# reader-hub threads (net/reader.py; readerhub.inc set_readers). One: at 64
-# namespace watches on the box's 16-CPU share two readers took the reader
-# thread off the bound (recv 0.97 -> 0.8-0.97 over two) but the loop then
-# saturated (0.97-0.99) and the decode workers, sharing cores with the second
-# reader, ran slower: 2.30-2.42M against 2.31-2.53M with one
-# (profiles/r6/readers). More pays only where the loop has room.
-HUB_READERS = 1
+# reader-hub threads (net/reader.py; readerhub.inc set_readers): 0 = auto
+# (utils/cpus.py auto_reader_threads: two for several watch scopes on a CPU
+# share of 12+, else one)
+HUB_READERS = 0
+# read-ahead over all streams when there are several watch scopes and
+# watcher.watch_reader_max_bytes is 0: with the whole pool (256 MiB) the
+# namespace watches' buffers waited 13-28 ms for the loop and were out of the
+# L3 by then, and the pool ran short (starved streams); 8 MiB keeps them young.
+# 64 namespaces, interleaved on the box: 2.45-2.54M (one reader, the pool),
+# 2.59-2.94M (one reader, 8 MiB), 3.05-3.13M (two readers, 8 MiB)
+# (profiles/r6/readers/final). One cluster-wide watch keeps the pool: its two
+# buffers of 4 MiB are its read-ahead anyway.
+HUB_MULTI_READ_AHEAD = 8 << 20
 MALLOC_TRIM_MIN_FREE = 16 << 20  # a periodic malloc_trim runs only when the C heap keeps this much free
 SPOOL_REPLAY_BATCH = 1000  # owed notifications re-submitted from the spool per replay pass
 
@@ -359,13 +365,14 @@ class WatcherService:
                                                        or getattr(http.ssl_context, "kw_tls", None) is not None):
                 # watch bodies read (and, for https, decrypted) on a native thread (net/reader.py)
                 from ..net.reader import WatchReaderHub
-                from ..utils.cpus import auto_tls_threads
+                from ..utils.cpus import auto_reader_threads, auto_tls_threads
                 self._reader_hub = WatchReaderHub(s.watcher.watch_read_bytes or (4 << 20),
                                                   s.watcher.watch_reader_buffers,
-                                                  max_bytes=s.watcher.watch_reader_max_bytes,
+                                                  max_bytes=(s.watcher.watch_reader_max_bytes or
+                                                             (HUB_MULTI_READ_AHEAD if self._multi else 0)),
                                                   frame=(HUB_FRAMING == "on" or
                                                          (HUB_FRAMING == "auto" and self._multi)),
-                                                  readers=HUB_READERS,
+                                                  readers=HUB_READERS or auto_reader_threads(self._multi),
                                                   tls_records=s.watcher.watch_tls_records == "native",
                                                   tls_threads=(s.watcher.watch_tls_threads
                                                                if s.watcher.watch_tls_threads >= 0

@@ -121,6 +121,17 @@ def auto_tls_threads(cpus: Optional[int] = None) -> int:
     return max(0, min(3, (cpus - 6) // 2))
 
 
+def auto_reader_threads(multi: bool, cpus: Optional[int] = None) -> int:
+    """Reader-hub threads (net/reader.py): one for a single cluster-wide
+    watch (one TCP stream is one thread's recv at most); with several watch
+    streams (namespace scopes) two where this process's share has room for
+    them beside the loop and the decode workers. With the read-ahead kept
+    small (engine/service.py HUB_MULTI_READ_AHEAD), 64 namespace watches ran
+    3.05-3.13M with two against 2.59-2.94M with one (profiles/r6/readers/final)."""
+    cpus = process_cpu_share() if cpus is None else cpus
+    return 2 if multi and cpus >= 12 else 1
+
+
 def auto_decode_spin_us(cpus: Optional[int] = None) -> float:
     """Idle spin of the decode workers before they sleep: 20 us when this
     process has CPUs to spare (a share of 8 or more), else 0. Workers still

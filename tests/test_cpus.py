@@ -172,3 +172,12 @@ def test_reader_core_split(tmp_path):
     reader, workers = reader_core_split(rest, root=str(tmp_path))
     assert reader == {1, 9} and workers == set(range(2, 8)) | set(range(10, 16))
     assert reader_core_split({1, 2, 3, 4, 9, 10, 11, 12}, root=str(tmp_path)) is None  # 3 cores left
+
+
+def test_auto_reader_threads():
+    """Two reader threads for several watch scopes on a CPU share of 12+,
+    one otherwise (a single watch stream is one thread's recv at most)."""
+    assert cpus.auto_reader_threads(False, 64) == 1
+    assert cpus.auto_reader_threads(True, 16) == 2
+    assert cpus.auto_reader_threads(True, 12) == 2
+    assert cpus.auto_reader_threads(True, 8) == 1

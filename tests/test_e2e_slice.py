@@ -202,6 +202,11 @@ def test_hub_framing_auto_follows_the_watch_shape(scope, framing, want, monkeypa
         srv, sink, svc = await start_stack(overrides={"watcher": {"namespace_scope": scope}})
         await svc.start()
         got = svc._reader_hub.frame
+        # the read-ahead follows the shape too: 8 MiB over several scopes, the pool for one watch
+        max_bytes = svc._reader_hub.core.stats()["max_bytes"]
+        assert max_bytes == (service.HUB_MULTI_READ_AHEAD if scope == "discover"
+                             else svc.settings.watcher.watch_reader_buffers * (svc.settings.watcher.watch_read_bytes
+                                                                               or (4 << 20))), max_bytes
         svc.stop()
         await svc.shutdown()
         await sink.stop()
